@@ -1,0 +1,152 @@
+// Fused AdamW over flat fp32 optimizer shards + gradient-norm helpers for gfx950.
+//
+// Replaces torch.optim.AdamW(foreach) (train_harness.py:329) and DeepSpeed's FusedAdam
+// multi_tensor_adam for the ZeRO paths.  All optimizer state lives in ONE flat fp32 "owner"
+// space per rank (the whole model for DDP, this rank's partition for ZeRO/FSDP), so a single
+// launch updates master weights, exp_avg and exp_avg_sq in one HBM pass and writes the bf16
+// compute copy of every parameter straight into its (possibly non-contiguous) destination:
+//
+//   segments: owner range [ostart, ostart + len) -> bf16 destination pointer
+//   blocks  : host-built table (segment id, owner start) so no block straddles a segment.
+//
+// Math is torch.optim.AdamW's:  p *= 1 - lr*wd;  m = lerp(m, g, 1-b1);  v = b2 v + (1-b2) g^2;
+//                                p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// with g optionally multiplied by a device-side scale (gradient clipping coefficient / 1/accum),
+// read from memory so no host sync is needed.
+#include "common.h"
+
+namespace {
+
+constexpr int kAdamThreads = 256;
+constexpr int kAdamIters = 4;
+constexpr int kAdamChunk = kAdamThreads * 4 * kAdamIters;   // elements per block
+
+template <typename G>
+DLTB_DEV void load4(const G* p, float* g);
+template <>
+DLTB_DEV void load4<float>(const float* p, float* g) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+}
+template <>
+DLTB_DEV void load4<bf16_t>(const bf16_t* p, float* g) {
+  uint2 v = *reinterpret_cast<const uint2*>(p);
+  g[0] = lo_bf(v.x); g[1] = hi_bf(v.x); g[2] = lo_bf(v.y); g[3] = hi_bf(v.y);
+}
+
+template <typename G>
+__global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
+    float* __restrict__ master, float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
+    const G* __restrict__ grad, const int* __restrict__ blk_seg, const int64_t* __restrict__ blk_start,
+    const int64_t* __restrict__ seg_ostart, const int64_t* __restrict__ seg_len,
+    const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, float lr, float beta1,
+    float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
+  const int seg = blk_seg[blockIdx.x];
+  const int64_t start = blk_start[blockIdx.x];
+  const int64_t seg_end = seg_ostart[seg] + seg_len[seg];
+  bf16_t* dst = reinterpret_cast<bf16_t*>(seg_dst[seg]);
+  const int64_t dst_base = start - seg_ostart[seg];
+  const float gs = gscale ? *gscale : 1.f;
+  const float decay = 1.f - lr * wd;
+#pragma unroll
+  for (int it = 0; it < kAdamIters; ++it) {
+    const int64_t off = (int64_t)it * kAdamThreads * 4 + threadIdx.x * 4;
+    const int64_t i = start + off;
+    if (i >= seg_end || off >= kAdamChunk) break;
+    float p[4], g[4], m[4], v[4];
+    load4<float>(master + i, p);
+    load4<float>(exp_avg + i, m);
+    load4<float>(exp_avg_sq + i, v);
+    load4<G>(grad + i, g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gg = g[e] * gs;
+      p[e] *= decay;
+      m[e] = m[e] + (1.f - beta1) * (gg - m[e]);
+      v[e] = beta2 * v[e] + (1.f - beta2) * gg * gg;
+      const float denom = sqrtf(v[e]) * inv_sqrt_bc2 + eps;
+      p[e] -= step_size * m[e] / denom;
+    }
+    *reinterpret_cast<float4*>(master + i) = make_float4(p[0], p[1], p[2], p[3]);
+    *reinterpret_cast<float4*>(exp_avg + i) = make_float4(m[0], m[1], m[2], m[3]);
+    *reinterpret_cast<float4*>(exp_avg_sq + i) = make_float4(v[0], v[1], v[2], v[3]);
+    uint2 o;
+    o.x = pack_bf2(p[0], p[1]);
+    o.y = pack_bf2(p[2], p[3]);
+    *reinterpret_cast<uint2*>(dst + dst_base + off) = o;
+  }
+}
+
+template <typename G>
+__global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ x, long n4,
+                                                   float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float g[4];
+    load4<G>(x + i * 4, g);
+    acc += g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) atomicAdd(out, acc);
+}
+
+// norm_sq[0] (already all-reduced) -> coef = min(1, max_norm / (sqrt(norm_sq) + 1e-6)), norm
+__global__ void clip_coef_kernel(const float* __restrict__ norm_sq, float max_norm,
+                                 float* __restrict__ coef, float* __restrict__ norm_out,
+                                 float extra_scale) {
+  const float nrm = sqrtf(norm_sq[0]) * extra_scale;
+  float c = max_norm > 0.f ? max_norm / (nrm + 1e-6f) : 1.f;
+  c = fminf(c, 1.f);
+  coef[0] = c * extra_scale;
+  if (norm_out) norm_out[0] = nrm;
+}
+
+__global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ x, long n, float v) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+
+}  // namespace
+
+int dltb_adamw_chunk() { return kAdamChunk; }
+
+void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* grad, bool grad_bf16,
+                const int* blk_seg, const int64_t* blk_start, int nblocks, const int64_t* seg_ostart,
+                const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, float lr,
+                float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2,
+                hipStream_t st) {
+  if (nblocks <= 0) return;
+  if (grad_bf16)
+    hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
+                       exp_avg, exp_avg_sq, (const bf16_t*)grad, blk_seg, blk_start, seg_ostart,
+                       seg_len, seg_dst, gscale, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
+  else
+    hipLaunchKernelGGL(adamw_kernel<float>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
+                       exp_avg, exp_avg_sq, (const float*)grad, blk_seg, blk_start, seg_ostart,
+                       seg_len, seg_dst, gscale, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
+}
+
+void dltb_sumsq(const void* x, bool bf16, long n, float* out, hipStream_t st) {
+  const long n4 = n / 4;
+  long g = (n4 + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  if (bf16)
+    hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, n4, out);
+  else
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, n4, out);
+}
+
+void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* norm_out,
+                    float extra_scale, hipStream_t st) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, st, norm_sq, max_norm, coef, norm_out,
+                     extra_scale);
+}
+
+void dltb_fill_f32(float* x, long n, float v, hipStream_t st) {
+  long g = (n + 255) / 256;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(fill_f32_kernel, dim3(g), dim3(256), 0, st, x, n, v);
+}

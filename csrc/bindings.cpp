@@ -1,0 +1,408 @@
+// pybind11 bindings of the dltb HIP kernels (module dltb._C).
+//
+// Thin adapters: validate devices/dtypes/shapes on the host (a wrong shape must never reach a
+// kernel: an out-of-bounds access can reset every GPU of the node), pick the current HIP stream,
+// and call the gfx950 launchers of launchers.h.  GEMMs stay in torch (hipBLASLt).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <cmath>
+
+#include "launchers.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+}
+void check_contig_bf16(const Tensor& t, const char* name) {
+  check_bf16(t, name);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_align16(const Tensor& t, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+              " must be 16-byte aligned");
+}
+
+uint32_t thr_of(double p) {
+  double t = p * 65536.0 + 0.5;
+  if (t > 65536.0) t = 65536.0;
+  return p > 0.0 ? (uint32_t)t : 0u;
+}
+float scale_of(double p) { return p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.f; }
+
+const int64_t* seed_ptr(const optional<Tensor>& seed, double p) {
+  if (p <= 0.0) return nullptr;
+  TORCH_CHECK(seed.has_value(), "dropout p > 0 needs a seed tensor");
+  check_cuda(*seed, "seed");
+  TORCH_CHECK(seed->scalar_type() == at::kLong && seed->numel() >= 1, "seed must be int64[1]");
+  return seed->data_ptr<int64_t>();
+}
+
+// ------------------------------------------------------------------------------------ norms
+std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& r, const Tensor& w,
+                             const optional<Tensor>& b, double eps, bool rms, double p,
+                             const optional<Tensor>& seed, int64_t site) {
+  check_contig_bf16(x, "x");
+  check_contig_bf16(w, "w");
+  const int64_t d = x.size(-1);
+  const int64_t N = x.numel() / d;
+  TORCH_CHECK(d % 8 == 0 && d <= 4096, "norm: d must be a multiple of 8 and <= 4096");
+  TORCH_CHECK(w.numel() == d, "norm: weight size");
+  if (!rms) {
+    TORCH_CHECK(b.has_value(), "layernorm needs a bias");
+    check_contig_bf16(*b, "b");
+    TORCH_CHECK(b->numel() == d, "norm: bias size");
+  }
+  Tensor s;
+  if (r.has_value()) {
+    check_contig_bf16(*r, "r");
+    TORCH_CHECK(r->sizes() == x.sizes(), "norm: residual shape");
+    s = at::empty_like(x);
+  }
+  auto y = at::empty_like(x);
+  auto fopt = x.options().dtype(at::kFloat);
+  auto mean = rms ? Tensor() : at::empty({N}, fopt);
+  auto rstd = at::empty({N}, fopt);
+  dltb_norm_fwd(x.data_ptr(), r.has_value() ? r->data_ptr() : nullptr, w.data_ptr(),
+                rms ? nullptr : b->data_ptr(), r.has_value() ? s.data_ptr() : nullptr,
+                y.data_ptr(), rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                (int)N, (int)d, (float)eps, rms, r.has_value() ? thr_of(p) : 0u, scale_of(p),
+                r.has_value() ? seed_ptr(seed, p) : nullptr, site, cur_stream());
+  return {s, y, mean, rstd};
+}
+
+Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const optional<Tensor>& mean,
+                const Tensor& rstd, const optional<Tensor>& dres, const Tensor& gw,
+                const optional<Tensor>& gb, bool accumulate, bool rms) {
+  check_contig_bf16(dy, "dy");
+  check_contig_bf16(s, "s");
+  check_contig_bf16(w, "w");
+  check_contig_bf16(gw, "gw");
+  const int64_t d = dy.size(-1);
+  const int64_t N = dy.numel() / d;
+  TORCH_CHECK(s.sizes() == dy.sizes() && w.numel() == d && gw.numel() == d, "norm_bwd shapes");
+  TORCH_CHECK(rstd.numel() == N, "norm_bwd: rstd size");
+  if (!rms) {
+    TORCH_CHECK(mean.has_value() && mean->numel() == N, "norm_bwd: mean");
+    TORCH_CHECK(gb.has_value(), "layernorm bwd needs gb");
+    check_contig_bf16(*gb, "gb");
+    TORCH_CHECK(gb->numel() == d, "norm_bwd: gb size");
+  }
+  if (dres.has_value()) {
+    check_contig_bf16(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == dy.sizes(), "norm_bwd: dres shape");
+  }
+  auto dx = at::empty_like(dy);
+  const int P = dltb_norm_bwd_partials((int)N);
+  auto part = at::empty({(int64_t)P * 2 * d}, dy.options().dtype(at::kFloat));
+  dltb_norm_bwd(dy.data_ptr(), s.data_ptr(), w.data_ptr(),
+                rms ? nullptr : mean->data_ptr<float>(), rstd.data_ptr<float>(),
+                dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(),
+                part.data_ptr<float>(), gw.data_ptr(), rms ? nullptr : gb->data_ptr(),
+                accumulate ? 1 : 0, (int)N, (int)d, rms, cur_stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------------------ elementwise
+Tensor gelu_fwd(const Tensor& f) {
+  check_contig_bf16(f, "f");
+  TORCH_CHECK(f.numel() % 8 == 0, "gelu: numel % 8");
+  auto g = at::empty_like(f);
+  dltb_gelu_fwd(f.data_ptr(), g.data_ptr(), f.numel(), cur_stream());
+  return g;
+}
+
+Tensor gelu_bwd(const Tensor& dg, const Tensor& f, const optional<Tensor>& db, bool accumulate) {
+  check_contig_bf16(dg, "dg");
+  check_contig_bf16(f, "f");
+  TORCH_CHECK(dg.sizes() == f.sizes(), "gelu_bwd shapes");
+  const int64_t k = f.size(-1);
+  const int64_t N = f.numel() / k;
+  TORCH_CHECK(k % 8 == 0, "gelu_bwd: k % 8");
+  if (db.has_value()) {
+    check_contig_bf16(*db, "db");
+    TORCH_CHECK(db->numel() == k, "gelu_bwd: db size");
+  }
+  auto df = at::empty_like(dg);
+  auto part = at::empty({(int64_t)dltb_colsum_partials((int)N) * k}, f.options().dtype(at::kFloat));
+  dltb_gelu_bwd(dg.data_ptr(), f.data_ptr(), df.data_ptr(), part.data_ptr<float>(),
+                db.has_value() ? db->data_ptr() : nullptr, accumulate ? 1 : 0, (int)N, (int)k,
+                cur_stream());
+  return df;
+}
+
+void colsum_into(const Tensor& src, const Tensor& out, bool accumulate) {
+  check_contig_bf16(src, "src");
+  check_contig_bf16(out, "out");
+  const int64_t k = src.size(-1);
+  const int64_t N = src.numel() / k;
+  TORCH_CHECK(out.numel() == k && k % 8 == 0, "colsum shapes");
+  auto part = at::empty({(int64_t)dltb_colsum_partials((int)N) * k}, src.options().dtype(at::kFloat));
+  dltb_colsum(src.data_ptr(), part.data_ptr<float>(), out.data_ptr(), accumulate ? 1 : 0, (int)N,
+              (int)k, cur_stream());
+}
+
+Tensor dropout(const optional<Tensor>& x, const Tensor& r, double p, const optional<Tensor>& seed,
+               int64_t site) {
+  check_contig_bf16(r, "r");
+  const int64_t cols = r.size(-1);
+  TORCH_CHECK(cols % 8 == 0, "dropout: last dim % 8");
+  if (x.has_value()) {
+    check_contig_bf16(*x, "x");
+    TORCH_CHECK(x->sizes() == r.sizes(), "dropout_add shapes");
+  }
+  auto out = at::empty_like(r);
+  dltb_dropout(x.has_value() ? x->data_ptr() : nullptr, r.data_ptr(), out.data_ptr(), r.numel(),
+               (int)cols, thr_of(p), scale_of(p), seed_ptr(seed, p), site, cur_stream());
+  return out;
+}
+
+Tensor swiglu_fwd(const Tensor& gu) {
+  check_contig_bf16(gu, "gu");
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "swiglu: 2F % 16");
+  const int64_t N = gu.numel() / F2;
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F2 / 2;
+  auto h = at::empty(sizes, gu.options());
+  dltb_swiglu_fwd(gu.data_ptr(), h.data_ptr(), (int)N, (int)(F2 / 2), cur_stream());
+  return h;
+}
+
+Tensor swiglu_bwd(const Tensor& dh, const Tensor& gu) {
+  check_contig_bf16(dh, "dh");
+  check_contig_bf16(gu, "gu");
+  const int64_t F2 = gu.size(-1);
+  const int64_t N = gu.numel() / F2;
+  TORCH_CHECK(dh.numel() == N * F2 / 2, "swiglu_bwd shapes");
+  auto dgu = at::empty_like(gu);
+  dltb_swiglu_bwd(dh.data_ptr(), gu.data_ptr(), dgu.data_ptr(), (int)N, (int)(F2 / 2), cur_stream());
+  return dgu;
+}
+
+void rope_(const Tensor& qkv, const Tensor& cosb, const Tensor& sinb, int64_t T, int64_t heads,
+           int64_t D, bool inverse) {
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "rope: qkv must be a 2-D row-major view");
+  check_cuda(cosb, "cos");
+  TORCH_CHECK(cosb.scalar_type() == at::kFloat && sinb.scalar_type() == at::kFloat, "rope tables f32");
+  TORCH_CHECK(cosb.is_contiguous() && sinb.is_contiguous(), "rope tables contiguous");
+  TORCH_CHECK(D % 16 == 0, "rope: D % 16");
+  TORCH_CHECK(cosb.numel() >= T * D / 2 && sinb.numel() >= T * D / 2, "rope table size");
+  TORCH_CHECK(qkv.size(1) >= heads * D, "rope: heads * D exceeds row");
+  const int64_t N = qkv.size(0);
+  TORCH_CHECK(N % T == 0, "rope: rows % T");
+  dltb_rope(qkv.data_ptr(), cosb.data_ptr<float>(), sinb.data_ptr<float>(), (int)N, (int)T,
+            (int)heads, (int)D, (int)qkv.stride(0), inverse, cur_stream());
+}
+
+void f32_from_bf16_(const Tensor& dst, const Tensor& src, bool accumulate) {
+  check_cuda(dst, "dst");
+  check_contig_bf16(src, "src");
+  TORCH_CHECK(dst.scalar_type() == at::kFloat && dst.is_contiguous(), "dst f32 contiguous");
+  TORCH_CHECK(dst.numel() == src.numel() && src.numel() % 8 == 0, "cast sizes");
+  check_align16(dst, "dst");
+  check_align16(src, "src");
+  dltb_f32_from_bf16(dst.data_ptr<float>(), src.data_ptr(), src.numel(), accumulate ? 1 : 0,
+                     cur_stream());
+}
+
+// ------------------------------------------------------------------------------ embedding
+Tensor embed_fwd(const Tensor& idx, const Tensor& wte, const Tensor& wpe, double p,
+                 const optional<Tensor>& seed, int64_t site) {
+  check_cuda(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 2 && idx.is_contiguous(), "idx [B,T] int64");
+  check_contig_bf16(wte, "wte");
+  check_contig_bf16(wpe, "wpe");
+  const int64_t B = idx.size(0), T = idx.size(1), d = wte.size(1);
+  TORCH_CHECK(wpe.size(1) == d && wpe.size(0) >= T && d % 8 == 0, "embed shapes");
+  auto x = at::empty({B, T, d}, wte.options());
+  dltb_embed_fwd(idx.data_ptr<int64_t>(), wte.data_ptr(), wpe.data_ptr(), x.data_ptr(), (int)(B * T),
+                 (int)T, (int)d, thr_of(p), scale_of(p), seed_ptr(seed, p), site, cur_stream());
+  return x;
+}
+
+// dwte must already hold whatever it accumulates onto (zero it when nothing was written yet)
+void embed_bwd(const Tensor& dx, const Tensor& idx, const optional<Tensor>& dwte,
+               const optional<Tensor>& dwpe, bool accumulate_wpe, double p,
+               const optional<Tensor>& seed, int64_t site) {
+  check_contig_bf16(dx, "dx");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 2, "idx [B,T] int64");
+  const int64_t B = idx.size(0), T = idx.size(1), d = dx.size(-1);
+  TORCH_CHECK(dx.numel() == B * T * d, "embed_bwd: dx shape");
+  const int64_t* sp = seed_ptr(seed, p);
+  if (dwpe.has_value()) {
+    check_contig_bf16(*dwpe, "dwpe");
+    TORCH_CHECK(dwpe->size(1) == d && dwpe->size(0) >= T, "embed_bwd: dwpe shape");
+    dltb_embed_bwd_pos(dx.data_ptr(), dwpe->data_ptr(), (int)B, (int)T, (int)dwpe->size(0), (int)d,
+                       accumulate_wpe ? 1 : 0, thr_of(p), scale_of(p), sp, site, cur_stream());
+  }
+  if (dwte.has_value()) {
+    check_contig_bf16(*dwte, "dwte");
+    TORCH_CHECK(dwte->size(1) == d, "embed_bwd: dwte shape");
+    auto flat = idx.reshape({-1}).contiguous();
+    auto sorted = at::sort(flat);
+    auto ids = std::get<0>(sorted).contiguous();
+    auto perm = std::get<1>(sorted).contiguous();
+    dltb_embed_bwd_tok(dx.data_ptr(), ids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
+                       dwte->data_ptr(), (int)(B * T), (int)d, thr_of(p), scale_of(p), sp, site,
+                       cur_stream());
+  }
+}
+
+// ------------------------------------------------------------------------------ xent
+Tensor xent_fwd_bwd_(const Tensor& logits, const Tensor& targets, int64_t ignore_index) {
+  check_contig_bf16(logits, "logits");
+  check_cuda(targets, "targets");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous(), "targets int64");
+  const int64_t V = logits.size(-1);
+  const int64_t N = logits.numel() / V;
+  TORCH_CHECK(targets.numel() == N, "xent: targets size");
+  TORCH_CHECK(V % 8 == 0 && V <= 131072, "xent: V % 8 and V <= 131072");
+  auto loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  dltb_xent_fwd_bwd(logits.data_ptr(), targets.data_ptr<int64_t>(), loss.data_ptr<float>(), (int)N,
+                    (int)V, ignore_index, cur_stream());
+  return loss;
+}
+
+// ------------------------------------------------------------------------------ optimizer
+void adamw(const Tensor& master, const Tensor& exp_avg, const Tensor& exp_avg_sq,
+           const Tensor& grad, const Tensor& blk_seg, const Tensor& blk_start,
+           const Tensor& seg_ostart, const Tensor& seg_len, const Tensor& seg_dst,
+           const optional<Tensor>& gscale, double lr, double beta1, double beta2, double eps,
+           double wd, int64_t step) {
+  for (auto* t : {&master, &exp_avg, &exp_avg_sq}) {
+    check_cuda(*t, "adam state");
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "adam state f32 contiguous");
+    check_align16(*t, "adam state");
+  }
+  check_cuda(grad, "grad");
+  TORCH_CHECK(grad.is_contiguous(), "grad contiguous");
+  TORCH_CHECK(master.numel() == exp_avg.numel() && master.numel() == exp_avg_sq.numel() &&
+                  master.numel() == grad.numel(), "adam: state sizes differ");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16, "grad dtype");
+  TORCH_CHECK(blk_seg.scalar_type() == at::kInt && blk_start.scalar_type() == at::kLong, "adam tables");
+  TORCH_CHECK(blk_seg.numel() == blk_start.numel(), "adam block tables");
+  TORCH_CHECK(step >= 1, "adam: step >= 1");
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const float* gs = nullptr;
+  if (gscale.has_value()) {
+    check_cuda(*gscale, "gscale");
+    TORCH_CHECK(gscale->scalar_type() == at::kFloat, "gscale f32");
+    gs = gscale->data_ptr<float>();
+  }
+  dltb_adamw(master.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(),
+             grad.data_ptr(), grad.scalar_type() == at::kBFloat16, blk_seg.data_ptr<int>(),
+             blk_start.data_ptr<int64_t>(), (int)blk_seg.numel(), seg_ostart.data_ptr<int64_t>(),
+             seg_len.data_ptr<int64_t>(), seg_dst.data_ptr<int64_t>(), gs, (float)lr, (float)beta1,
+             (float)beta2, (float)eps, (float)wd, (float)(lr / bc1), (float)(1.0 / std::sqrt(bc2)),
+             cur_stream());
+}
+
+void sumsq_(const Tensor& x, const Tensor& out) {
+  check_cuda(x, "x");
+  check_cuda(out, "out");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 4 == 0, "sumsq: contiguous, numel % 4");
+  TORCH_CHECK(out.scalar_type() == at::kFloat, "sumsq out f32");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "sumsq dtype");
+  dltb_sumsq(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(), out.data_ptr<float>(),
+             cur_stream());
+}
+
+void clip_coef(const Tensor& norm_sq, double max_norm, const Tensor& coef,
+               const optional<Tensor>& norm_out, double extra_scale) {
+  check_cuda(norm_sq, "norm_sq");
+  check_cuda(coef, "coef");
+  dltb_clip_coef(norm_sq.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(),
+                 norm_out.has_value() ? norm_out->data_ptr<float>() : nullptr, (float)extra_scale,
+                 cur_stream());
+}
+
+// ------------------------------------------------------------------------------ attention
+void check_attn_view(const Tensor& t, const char* name, int64_t rows, int64_t heads, int64_t D) {
+  check_bf16(t, name);
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be a 2-D row-major view [B*T, >=H*D]");
+  TORCH_CHECK(t.size(0) == rows && t.size(1) == heads * D, name, " shape mismatch");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8");
+  check_align16(t, name);
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, int64_t B,
+                             int64_t T, int64_t Hq, int64_t Hkv, double scale, bool causal,
+                             double p, const optional<Tensor>& seed, int64_t site) {
+  const int64_t D = q.size(1) / Hq;
+  TORCH_CHECK(dltb_attn_supported((int)D, (int)T), "attention: needs D in {64,128} and T % 128 == 0");
+  TORCH_CHECK(Hq % Hkv == 0, "attention: Hq % Hkv");
+  check_attn_view(q, "q", B * T, Hq, D);
+  check_attn_view(k, "k", B * T, Hkv, D);
+  check_attn_view(v, "v", B * T, Hkv, D);
+  dltb_attn_init_attributes();
+  auto o = at::empty({B * T, Hq * D}, q.options());
+  auto lse = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
+  dltb_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                q.stride(0), k.stride(0), v.stride(0), o.stride(0), (int)B, (int)T, (int)Hq,
+                (int)Hkv, (int)D, (float)scale, causal ? 1 : 0, thr_of(p), scale_of(p),
+                seed_ptr(seed, p), site, cur_stream());
+  return {o, lse};
+}
+
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,
+              const Tensor& lse, const Tensor& dq, const Tensor& dk, const Tensor& dv, int64_t B,
+              int64_t T, int64_t Hq, int64_t Hkv, double scale, bool causal, double p,
+              const optional<Tensor>& seed, int64_t site) {
+  const int64_t D = q.size(1) / Hq;
+  TORCH_CHECK(dltb_attn_supported((int)D, (int)T), "attention: needs D in {64,128} and T % 128 == 0");
+  check_attn_view(q, "q", B * T, Hq, D);
+  check_attn_view(k, "k", B * T, Hkv, D);
+  check_attn_view(v, "v", B * T, Hkv, D);
+  check_attn_view(o, "o", B * T, Hq, D);
+  check_attn_view(dout, "dout", B * T, Hq, D);
+  check_attn_view(dq, "dq", B * T, Hq, D);
+  check_attn_view(dk, "dk", B * T, Hkv, D);
+  check_attn_view(dv, "dv", B * T, Hkv, D);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == B * Hq * T && lse.is_contiguous(), "lse");
+  dltb_attn_init_attributes();
+  auto delta = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
+  dltb_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
+                lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
+                dv.data_ptr(), q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0),
+                dq.stride(0), dk.stride(0), dv.stride(0), (int)B, (int)T, (int)Hq, (int)Hkv, (int)D,
+                (float)scale, causal ? 1 : 0, thr_of(p), scale_of(p), seed_ptr(seed, p), site,
+                cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "dltb gfx950 (MI355X) HIP kernels";
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("colsum_into", &colsum_into);
+  m.def("dropout", &dropout);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope_", &rope_);
+  m.def("f32_from_bf16_", &f32_from_bf16_);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("xent_fwd_bwd_", &xent_fwd_bwd_);
+  m.def("adamw", &adamw);
+  m.def("adamw_chunk", &dltb_adamw_chunk);
+  m.def("sumsq_", &sumsq_);
+  m.def("clip_coef", &clip_coef);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("arch", []() { return std::string("gfx950"); });
+}

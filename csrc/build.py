@@ -1,0 +1,121 @@
+#!/usr/bin/env python3
+"""Build the dltb._C extension in-tree for gfx950 (MI355X).
+
+Explicit toolchain, no hipify, no JIT cache: every ``csrc/*.hip`` kernel file is compiled by
+``hipcc --offload-arch=gfx950`` without torch headers (seconds per file, in parallel), the
+pybind11/ATen adapter ``bindings.cpp`` by the host compiler against the installed PyTorch-ROCm
+headers, and everything is linked into
+``distributed-llm-training-benchmark-framework_amd/_C.<EXT_SUFFIX>`` next to the Python sources,
+so the built ``.so`` travels with the repository snapshot to the GPU box.
+
+Usage:  python csrc/build.py [--force] [--debug] [-j N]
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PKG_DIR = os.path.join(ROOT, "distributed-llm-training-benchmark-framework_amd")
+BUILD_DIR = os.path.join(ROOT, "build", "csrc")
+ARCH = os.environ.get("DLTB_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def ext_path() -> str:
+    return os.path.join(PKG_DIR, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _headers():
+    return glob.glob(os.path.join(HERE, "*.h"))
+
+
+def _stale(obj, src, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(p) > t for p in [src] + deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed:\n  " + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+    incs = ce.include_paths(device_type="cuda") if "device_type" in ce.include_paths.__code__.co_varnames \
+        else ce.include_paths(cuda=True)
+    incs = list(dict.fromkeys(incs + [sysconfig.get_paths()["include"], os.path.join(ROCM, "include")]))
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    flags = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+             "-DHIPBLAS_V2", "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C"]
+    for fn in ():
+        f = getattr(ce, fn, None)
+        if f is not None:
+            try:
+                flags += list(f())
+            except Exception:
+                pass
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    return incs, flags, libdir
+
+
+def build(force: bool = False, debug: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    hdrs = _headers()
+    opt = ["-O0", "-g", "-DDLTB_DEBUG=1"] if debug else ["-O3"]
+    hip_srcs = sorted(glob.glob(os.path.join(HERE, "*.hip")))
+    jobs_list = []
+    objs = []
+    for src in hip_srcs:
+        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src, hdrs):
+            jobs_list.append([hipcc, "-c", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", *opt,
+                              "-munsafe-fp-atomics", "-I", HERE, src, "-o", obj])
+    incs, tflags, libdir = _torch_flags()
+    bsrc = os.path.join(HERE, "bindings.cpp")
+    bobj = os.path.join(BUILD_DIR, "bindings.cpp.o")
+    objs.append(bobj)
+    if force or _stale(bobj, bsrc, hdrs):
+        jobs_list.append([cxx, "-c", "-fPIC", "-std=c++17", "-O2", *tflags,
+                          *[f"-I{p}" for p in incs], "-I", HERE, bsrc, "-o", bobj])
+    out = ext_path()
+    if jobs_list:
+        if verbose:
+            print(f"[dltb.build] compiling {len(jobs_list)} translation unit(s) for {ARCH}", flush=True)
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            for _ in ex.map(_run, jobs_list):
+                pass
+    if jobs_list or not os.path.exists(out) or any(os.path.getmtime(o) > os.path.getmtime(out) for o in objs):
+        link = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, f"-L{libdir}",
+                "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+                f"-Wl,-rpath,{libdir}", "-o", out]
+        _run(link)
+        if verbose:
+            print(f"[dltb.build] linked {out}", flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    a = ap.parse_args()
+    build(force=a.force, debug=a.debug, jobs=a.jobs)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,70 @@
+// Host launch entry points of the dltb HIP kernels (implemented in csrc/*.hip, compiled by hipcc
+// for gfx950 without torch headers; bindings.cpp adapts them to at::Tensor).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+// norm.hip
+void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, void* s_out,
+                   void* y, float* mean, float* rstd, int N, int d, float eps, bool rms,
+                   uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
+                   hipStream_t st);
+int dltb_norm_bwd_partials(int N);
+void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
+                   const float* rstd, const void* dres, void* dx, float* part, void* gw, void* gb,
+                   int accumulate, int N, int d, bool rms, hipStream_t st);
+
+// elementwise.hip
+void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st);
+int dltb_colsum_partials(int N);
+void dltb_gelu_bwd(const void* dg, const void* f, void* df, float* part, void* db, int accumulate,
+                   int N, int k, hipStream_t st);
+void dltb_colsum(const void* src, float* part, void* out, int accumulate, int N, int k,
+                 hipStream_t st);
+void dltb_dropout(const void* x, const void* r, void* out, long n, int cols, uint32_t thr16,
+                  float scale, const int64_t* seed, int64_t site, hipStream_t st);
+void dltb_swiglu_fwd(const void* gu, void* h, int N, int F, hipStream_t st);
+void dltb_swiglu_bwd(const void* dh, const void* gu, void* dgu, int N, int F, hipStream_t st);
+void dltb_rope(void* qkv, const float* cosb, const float* sinb, int N, int T, int heads, int D,
+               int stride, bool inverse, hipStream_t st);
+void dltb_f32_from_bf16(float* dst, const void* src, long n, int accumulate, hipStream_t st);
+
+// embedding.hip
+void dltb_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* x, int N, int T,
+                    int d, uint32_t thr16, float scale, const int64_t* seed, int64_t site,
+                    hipStream_t st);
+void dltb_embed_bwd_pos(const void* dx, void* dwpe, int B, int T, int P, int d, int accumulate,
+                        uint32_t thr16, float scale, const int64_t* seed, int64_t site,
+                        hipStream_t st);
+void dltb_embed_bwd_tok(const void* dx, const int64_t* sorted_ids, const int64_t* perm,
+                        void* dwte, int N, int d, uint32_t thr16, float scale,
+                        const int64_t* seed, int64_t site, hipStream_t st);
+
+// xent.hip
+void dltb_xent_fwd_bwd(void* logits, const int64_t* targets, float* loss, int N, int V,
+                       int64_t ignore_index, hipStream_t st);
+
+// adamw.hip
+int dltb_adamw_chunk();
+void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* grad, bool grad_bf16,
+                const int* blk_seg, const int64_t* blk_start, int nblocks, const int64_t* seg_ostart,
+                const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, float lr,
+                float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2,
+                hipStream_t st);
+void dltb_sumsq(const void* x, bool bf16, long n, float* out, hipStream_t st);
+void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* norm_out,
+                    float extra_scale, hipStream_t st);
+void dltb_fill_f32(float* x, long n, float v, hipStream_t st);
+
+// attention.hip
+bool dltb_attn_supported(int D, int T);
+void dltb_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, long qs,
+                   long ks, long vs, long os, int B, int T, int Hq, int Hkv, int D, float scale,
+                   int causal, uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
+                   hipStream_t st);
+void dltb_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                   const float* lse, float* delta, void* dq, void* dk, void* dv, long qs, long ks,
+                   long vs, long os, long dos, long dqs, long dks, long dvs, int B, int T, int Hq,
+                   int Hkv, int D, float scale, int causal, uint32_t thr16, float drop_scale,
+                   const int64_t* seed, int64_t site, hipStream_t st);
+void dltb_attn_init_attributes();

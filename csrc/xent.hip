@@ -1,0 +1,87 @@
+// Fused softmax cross-entropy forward + backward for gfx950 (F.cross_entropy with
+// ignore_index, train_harness.py:99-103).
+//
+// One 512-thread workgroup per row; the whole bf16 row (V = 32000 -> 8 x 16-byte vectors per
+// thread) stays in registers, so logits are read from HBM exactly once:
+//     loss[r]      = logsumexp(z_r) - z_r[t_r]              (0 for ignored rows)
+//     z_r (in place) <- softmax(z_r) - onehot(t_r)           (unscaled dlogits; 0 for ignored)
+// The 1/count mean-reduction and the incoming grad_output are applied by the caller as a device
+// scalar folded into the head GEMMs, so no host sync is needed anywhere.
+#include "common.h"
+
+namespace {
+
+template <int VPT>
+__global__ __launch_bounds__(512) void xent_kernel(bf16_t* __restrict__ logits,
+                                                  const int64_t* __restrict__ targets,
+                                                  float* __restrict__ loss, int V,
+                                                  int64_t ignore_index) {
+  __shared__ float red[8];
+  __shared__ float s_tlogit;
+  const int row = blockIdx.x;
+  bf16_t* z = logits + (long)row * V;
+  const int64_t t = targets[row];
+  const bool valid = (t != ignore_index) && t >= 0 && t < V;
+  if (threadIdx.x == 0) s_tlogit = valid ? bf2f(z[t]) : 0.f;
+  const int nvec = V >> 3;
+  uint4 v[VPT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int i = j * 512 + threadIdx.x;
+    if (i < nvec) {
+      v[j] = ld16<uint4>(z + i * 8);
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, f[e]);
+    }
+  }
+  m = block_max(m, red);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int i = j * 512 + threadIdx.x;
+    if (i < nvec) {
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += __expf(f[e] - m);
+    }
+  }
+  s = block_sum(s, red);
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) loss[row] = valid ? (m + __logf(s) - s_tlogit) : 0.f;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int i = j * 512 + threadIdx.x;
+    if (i < nvec) {
+      float f[8];
+      unpack8(v[j], f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float p = valid ? __expf(f[e] - m) * inv : 0.f;
+        if (valid && i * 8 + e == t) p -= 1.f;
+        f[e] = p;
+      }
+      *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
+    }
+  }
+}
+
+}  // namespace
+
+void dltb_xent_fwd_bwd(void* logits, const int64_t* targets, float* loss, int N, int V,
+                       int64_t ignore_index, hipStream_t st) {
+  const int vpt = cdiv(V / 8, 512);
+#define DLTB_XE(K)                                                                              \
+  hipLaunchKernelGGL(xent_kernel<K>, dim3(N), dim3(512), 0, st, (bf16_t*)logits, targets, loss, \
+                     V, ignore_index)
+  if (vpt <= 1) DLTB_XE(1);
+  else if (vpt <= 2) DLTB_XE(2);
+  else if (vpt <= 4) DLTB_XE(4);
+  else if (vpt <= 8) DLTB_XE(8);
+  else if (vpt <= 16) DLTB_XE(16);
+  else DLTB_XE(32);
+#undef DLTB_XE
+}

@@ -1,0 +1,253 @@
+"""Numerics of every gfx950 HIP kernel against a plain-torch fp32 reference of the same op.
+
+The references live in dltb.ops.ref and share the dropout counter hash with the kernels, so
+dropout masks must match exactly (any mask mismatch shows up as O(1) errors).
+"""
+import math
+
+import pytest
+import torch
+
+import dltb
+from dltb.ops import ref
+from dltb.ops._ext import ext
+from dltb.ops.rng import StepSeed
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def close(a, b, atol, rtol, what=""):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).float().mean().item()
+    assert bad == 0.0, f"{what}: {bad*100:.3f}% elements out of tolerance, max err {err.max().item():.4g}"
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*shape, device=DEV) * scale).to(dtype)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _ext_loaded():
+    C = ext()
+    assert C.arch() == "gfx950"
+    torch.manual_seed(0)
+
+
+def seed_obj(v=1234):
+    s = StepSeed(v, 0, device=DEV)
+    s.next()
+    return s
+
+
+# ------------------------------------------------------------------------------ norms
+@pytest.mark.parametrize("d", [64, 768, 1024, 2048, 4096])
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("res_p", [None, 0.0, 0.1])
+def test_norm_fwd_bwd(d, rms, res_p):
+    N = 300
+    x, w, b = rnd(N, d), rnd(d, scale=0.5) + 1, rnd(d, scale=0.1)
+    r = rnd(N, d) if res_p is not None else None
+    p = res_p or 0.0
+    sd = seed_obj()
+    C = ext()
+    s, y, mean, rstd = C.norm_fwd(x, r, w, None if rms else b, 1e-5, rms, p, sd.device_tensor, 3)
+    rs, ry, rmean, rrstd = ref.norm_fwd(x, r, w, None if rms else b, 1e-5, rms, p, sd, 3)
+    if r is not None:
+        close(s, rs, 1e-2, 1e-2, "s")
+    close(y, ry, 2e-2, 2e-2, "y")
+    close(rstd, rrstd, 1e-4, 1e-3, "rstd")
+    # backward
+    dy = rnd(N, d)
+    dres = rnd(N, d) if r is not None else None
+    sin = s if r is not None else x
+    gw = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
+    gb = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
+    rgw, rgb = gw.clone(), gb.clone()
+    dx = C.norm_bwd(dy, sin, w, None if rms else mean, rstd, dres, gw, None if rms else gb, False, rms)
+    rdx = ref.norm_bwd(dy, sin, w, rmean, rrstd, dres, rgw, rgb, False, rms)
+    close(dx, rdx, 3e-2, 3e-2, "dx")
+    close(gw, rgw, 0.15, 2e-2, "dgamma")
+    if not rms:
+        close(gb, rgb, 0.15, 2e-2, "dbeta")
+    # accumulate mode adds onto the slot
+    gw2 = gw.clone()
+    C.norm_bwd(dy, sin, w, None if rms else mean, rstd, dres, gw2, None if rms else gb.clone(), True, rms)
+    close(gw2, 2 * gw.float(), 0.3, 3e-2, "dgamma accumulate")
+
+
+# ------------------------------------------------------------------------------ elementwise
+def test_gelu_and_bias_grad():
+    N, k = 512, 4096
+    f = rnd(N, k)
+    C = ext()
+    close(C.gelu_fwd(f), ref.gelu_fwd(f), 1e-2, 1e-2, "gelu")
+    dg = rnd(N, k)
+    db = torch.zeros(k, device=DEV, dtype=torch.bfloat16)
+    rdb = db.clone()
+    df = C.gelu_bwd(dg, f, db, False)
+    rdf = ref.gelu_bwd(dg, f, rdb, False)
+    close(df, rdf, 1e-2, 2e-2, "dgelu")
+    close(db, rdb, 0.2, 2e-2, "gelu bias grad")
+
+
+def test_colsum_and_dropout():
+    C = ext()
+    src = rnd(1000, 3072)
+    out = rnd(3072)
+    expect = out.float() + src.float().sum(0)
+    C.colsum_into(src, out, True)
+    close(out, expect, 0.3, 2e-2, "colsum accumulate")
+    sd = seed_obj(99)
+    x, r = rnd(257, 1024), rnd(257, 1024)
+    y = C.dropout(x, r, 0.1, sd.device_tensor, 7)
+    ry = ref.dropout(x, r, 0.1, sd, 7)
+    close(y, ry, 1e-2, 1e-2, "dropout_add")
+    kept = (C.dropout(None, torch.ones_like(r), 0.1, sd.device_tensor, 7).float() > 0).float().mean().item()
+    assert abs(kept - 0.9) < 0.01
+
+
+def test_swiglu_rope():
+    C = ext()
+    gu = rnd(256, 2 * 512)
+    close(C.swiglu_fwd(gu), ref.swiglu_fwd(gu), 1e-2, 2e-2, "swiglu")
+    dh = rnd(256, 512)
+    close(C.swiglu_bwd(dh, gu), ref.swiglu_bwd(dh, gu), 1e-2, 3e-2, "swiglu bwd")
+    T, Hq, Hkv, D = 128, 4, 2, 128
+    qkv = rnd(2 * T, (Hq + 2 * Hkv) * D)
+    cos, sin = ref.rope_tables(T, D, 10000.0, DEV)
+    a, b = qkv.clone(), qkv.clone()
+    C.rope_(a, cos, sin, T, Hq + Hkv, D, False)
+    ref.rope_(b, cos, sin, T, Hq + Hkv, D, False)
+    close(a, b, 1e-2, 1e-2, "rope")
+    C.rope_(a, cos, sin, T, Hq + Hkv, D, True)
+    close(a, qkv, 3e-2, 3e-2, "rope inverse")
+
+
+def test_embedding():
+    C = ext()
+    V, d, B, T = 1000, 256, 2, 128
+    wte, wpe = rnd(V, d), rnd(T, d)
+    idx = torch.randint(0, 50, (B, T), device=DEV)   # many repeated ids
+    sd = seed_obj(5)
+    x = C.embed_fwd(idx, wte, wpe, 0.1, sd.device_tensor, 0)
+    close(x, ref.embed_fwd(idx, wte, wpe, 0.1, sd, 0), 1e-2, 1e-2, "embed fwd")
+    dx = rnd(B, T, d)
+    dwte, dwpe = rnd(V, d), torch.zeros(T, d, device=DEV, dtype=torch.bfloat16)
+    rdwte, rdwpe = dwte.clone(), dwpe.clone()
+    C.embed_bwd(dx, idx, dwte, dwpe, False, 0.1, sd.device_tensor, 0)
+    ref.embed_bwd(dx, idx, rdwte, rdwpe, False, 0.1, sd, 0)
+    close(dwpe, rdwpe, 2e-2, 2e-2, "dwpe")
+    close(dwte, rdwte, 5e-2, 2e-2, "dwte")
+
+
+def test_xent():
+    C = ext()
+    N, V = 300, 32000
+    logits = rnd(N, V, scale=2.0)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[::7] = -1
+    a, b = logits.clone(), logits.clone()
+    la = C.xent_fwd_bwd_(a, tgt, -1)
+    lb = ref.xent_fwd_bwd_(b, tgt, -1)
+    close(la, lb, 1e-3, 1e-3, "xent loss")
+    close(a, b, 1e-4, 2e-2, "dlogits")
+    # against torch's own cross entropy
+    valid = tgt != -1
+    want = torch.nn.functional.cross_entropy(logits.float(), tgt, ignore_index=-1)
+    got = la.sum() / valid.sum()
+    assert abs(got.item() - want.item()) < 1e-3
+
+
+# ------------------------------------------------------------------------------ attention
+ATTN_CASES = [
+    # B, T, Hq, Hkv, D, causal, p
+    (2, 256, 4, 4, 64, False, 0.0),
+    (2, 256, 4, 4, 64, False, 0.1),
+    (1, 512, 2, 2, 64, True, 0.0),
+    (1, 256, 8, 2, 128, True, 0.0),
+    (1, 256, 4, 4, 128, False, 0.1),
+]
+
+
+@pytest.mark.parametrize("B,T,Hq,Hkv,D,causal,p", ATTN_CASES)
+def test_attention(B, T, Hq, Hkv, D, causal, p):
+    C = ext()
+    W = (Hq + 2 * Hkv) * D
+    qkv = rnd(B * T, W)
+    q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
+    scale = 1.0 / math.sqrt(D)
+    sd = seed_obj(42)
+    o, lse = C.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, sd.device_tensor if p else None, 11)
+    ro, rlse = ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, sd, 11)
+    close(lse, rlse, 2e-3, 1e-3, "lse")
+    close(o, ro, 2e-2, 3e-2, "O")
+    do = rnd(B * T, Hq * D)
+    dqkv = torch.empty_like(qkv)
+    rdqkv = torch.empty_like(qkv)
+    sl = lambda t: (t[:, :Hq * D], t[:, Hq * D:(Hq + Hkv) * D], t[:, (Hq + Hkv) * D:])
+    C.attn_bwd(q, k, v, o, do, lse, *sl(dqkv), B, T, Hq, Hkv, scale, causal, p,
+               sd.device_tensor if p else None, 11)
+    ref.attn_bwd(q, k, v, o, do, lse, *sl(rdqkv), B, T, Hq, Hkv, scale, causal, p, sd, 11)
+    for name, a, b in zip("qkv", sl(dqkv), sl(rdqkv)):
+        close(a, b, 5e-2, 5e-2, "d" + name)
+
+
+def test_attention_tinygpt_shape():
+    """Tier-A shape: T=2048, 16 heads, D=64, non-causal, dropout 0.1 (fwd only vs fp32)."""
+    C = ext()
+    B, T, H, D = 1, 2048, 16, 64
+    qkv = rnd(B * T, 3 * H * D)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    sd = seed_obj(3)
+    o, lse = C.attn_fwd(q, k, v, B, T, H, H, 0.125, False, 0.1, sd.device_tensor, 1)
+    ro, rlse = ref.attn_fwd(q, k, v, B, T, H, H, 0.125, False, 0.1, sd, 1)
+    close(o, ro, 2e-2, 3e-2, "O tier A")
+
+
+# ------------------------------------------------------------------------------ optimizer
+def _adam_tables(n, dst, chunk):
+    nb = (n + chunk - 1) // chunk
+    blk_seg = torch.zeros(nb, dtype=torch.int32, device=DEV)
+    blk_start = torch.arange(nb, dtype=torch.int64, device=DEV) * chunk
+    so = torch.zeros(1, dtype=torch.int64, device=DEV)
+    sl = torch.tensor([n], dtype=torch.int64, device=DEV)
+    sdst = torch.tensor([dst.data_ptr()], dtype=torch.int64, device=DEV)
+    return blk_seg, blk_start, so, sl, sdst
+
+
+@pytest.mark.parametrize("gdtype", [torch.float32, torch.bfloat16])
+def test_adamw_matches_torch(gdtype):
+    C = ext()
+    n = 100_000
+    p0 = torch.randn(n, device=DEV)
+    master, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    out_bf16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    tp = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.AdamW([tp], lr=1e-3, weight_decay=0.01)
+    tabs = _adam_tables(n, out_bf16, C.adamw_chunk())
+    for step in range(1, 4):
+        g = torch.randn(n, device=DEV).to(gdtype)
+        tp.grad = g.float()
+        opt.step()
+        C.adamw(master, m, v, g, *tabs, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+    close(master, tp.detach(), 1e-6, 1e-5, "adamw master")
+    close(out_bf16, tp.detach().to(torch.bfloat16), 1e-2, 1e-2, "adamw bf16 copy")
+
+
+def test_sumsq_clip():
+    C = ext()
+    x = torch.randn(1 << 20, device=DEV)
+    acc = torch.zeros(1, device=DEV)
+    C.sumsq_(x, acc)
+    C.sumsq_(x.to(torch.bfloat16), acc)
+    want = 2 * (x.double() ** 2).sum().item()
+    assert abs(acc.item() - want) / want < 1e-3
+    coef = torch.zeros(1, device=DEV)
+    nrm = torch.zeros(1, device=DEV)
+    C.clip_coef(acc, 1.0, coef, nrm, 1.0)
+    assert abs(nrm.item() - math.sqrt(want)) / math.sqrt(want) < 1e-3
+    assert abs(coef.item() - 1.0 / (math.sqrt(want) + 1e-6)) < 1e-6
