@@ -1,0 +1,278 @@
+"""TinyGPT — the reference benchmark model, re-built as fused per-unit autograd Functions.
+
+Reference: ``benchmarking/train_harness.py:36-131`` (TinyGPT + TransformerBlock).  Parameter names,
+shapes, tying and initialisation match the reference exactly so state dicts are interchangeable:
+
+    transformer.wte.weight [V, d]  (tied with lm_head.weight)     transformer.wpe.weight [block, d]
+    transformer.h.{i}.ln_1.{weight,bias}   .attn.in_proj_{weight [3d, d], bias [3d]}
+    transformer.h.{i}.attn.out_proj.{weight, bias}   .ln_2.{weight,bias}
+    transformer.h.{i}.mlp.0.{weight [4d, d], bias}   .mlp.2.{weight [d, 4d], bias}
+    transformer.ln_f.{weight,bias}
+
+Semantics reproduced from the reference: NON-causal attention (no mask), dropout
+p on the embedding sum, the attention probabilities and the MLP output, pre-LN blocks, exact-erf
+GELU, learned absolute positions, tied head, ``cross_entropy(ignore_index=-1)``.  Dead work of the
+reference is not performed: ``ln_1`` is evaluated once (it is called 3x on the same input at
+``train_harness.py:127``) and the head-averaged attention weights (``need_weights=True``) are never
+computed.  The fused head returns ``logits=None`` when a loss is requested (the logits buffer is
+overwritten by the softmax-xent gradient in place); pass ``return_logits=True`` to get them.
+
+Per block (N = B*T tokens):  h1 = LN1(x); qkv = h1 Win^T + b; o = FlashAttn(qkv); a = o Wo^T + b;
+x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g W2^T + b;
+x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as F_
+from ..parallel.runtime import EAGER, Unit
+from .config import ModelConfig
+
+LN_EPS = 1e-5
+
+
+class _MHAParams(nn.Module):
+    """Parameter container with nn.MultiheadAttention's names (in_proj_weight, out_proj.*)."""
+
+    def __init__(self, d):
+        super().__init__()
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * d))
+        self.out_proj = nn.Linear(d, d)
+        nn.init.xavier_uniform_(self.in_proj_weight)    # nn.MultiheadAttention._reset_parameters
+        nn.init.zeros_(self.out_proj.bias)
+
+
+class TinyGPTBlock(nn.Module):
+    def __init__(self, d, n_head, dropout):
+        super().__init__()
+        self.ln_1 = nn.LayerNorm(d)
+        self.attn = _MHAParams(d)
+        self.ln_2 = nn.LayerNorm(d)
+        self.mlp = nn.Sequential(nn.Linear(d, 4 * d), nn.GELU(), nn.Linear(4 * d, d), nn.Dropout(dropout))
+
+    def param_list(self):
+        return [("ln_1.weight", self.ln_1.weight), ("ln_1.bias", self.ln_1.bias),
+                ("attn.in_proj_weight", self.attn.in_proj_weight), ("attn.in_proj_bias", self.attn.in_proj_bias),
+                ("attn.out_proj.weight", self.attn.out_proj.weight), ("attn.out_proj.bias", self.attn.out_proj.bias),
+                ("ln_2.weight", self.ln_2.weight), ("ln_2.bias", self.ln_2.bias),
+                ("mlp.0.weight", self.mlp[0].weight), ("mlp.0.bias", self.mlp[0].bias),
+                ("mlp.2.weight", self.mlp[2].weight), ("mlp.2.bias", self.mlp[2].bias)]
+
+
+# ============================================================================ fused Functions
+class _EmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, idx, model):
+        rt, unit = model.rt, model.unit_embed
+        wte, wpe = rt.acquire(unit)
+        p = model.drop_p
+        x = F_.embed_fwd(idx, wte, wpe, p, rt.seed, model.site_embed)
+        rt.release_forward(unit)
+        ctx.model, ctx.idx = model, idx
+        return x.view(-1, x.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dx):
+        model = ctx.model
+        rt, unit = model.rt, model.unit_embed
+        rt.acquire_backward(unit)
+        dwte, acc_wte = rt.grad_slot(unit, 0)
+        dwpe, acc_wpe = rt.grad_slot(unit, 1)
+        if not acc_wte:
+            dwte.zero_()
+        F_.embed_bwd(dx.contiguous(), ctx.idx, dwte, dwpe, acc_wpe, model.drop_p, rt.seed, model.site_embed)
+        rt.grads_ready(unit)
+        rt.release_backward(unit)
+        return None, None, None
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, model, i):
+        rt, unit = model.rt, model.unit_blocks[i]
+        (ln1w, ln1b, win, bin_, wo, bo, ln2w, ln2b, w1, b1, w2, b2) = rt.acquire(unit)
+        B, T = model._cur_bt
+        cfg = model.cfg
+        H, d = cfg.n_head, cfg.n_embd
+        p = model.drop_p
+        _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False)
+        qkv = F_.linear_fwd(h1, win, bin_)
+        o, lse = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
+                             1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
+        a = F_.linear_fwd(o, wo, bo)
+        x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False)
+        f = F_.linear_fwd(h2, w1, b1)
+        g = F_.gelu_fwd(f)
+        m = F_.linear_fwd(g, w2, b2)
+        x2 = F_.dropout(x1, m, p, rt.seed, model.site_mlp(i))
+        rt.release_forward(unit)
+        ctx.model, ctx.i = model, i
+        ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, x1, h2, mean2, rstd2, f, g)
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        model, i = ctx.model, ctx.i
+        rt, unit = model.rt, model.unit_blocks[i]
+        (x, h1, mean1, rstd1, qkv, o, lse, x1, h2, mean2, rstd2, f, g) = ctx.saved
+        ctx.saved = None
+        (ln1w, ln1b, win, bin_, wo, bo, ln2w, ln2b, w1, b1, w2, b2) = rt.acquire_backward(unit)
+        B, T = model._cur_bt
+        cfg = model.cfg
+        H, d = cfg.n_head, cfg.n_embd
+        p = model.drop_p
+        dx2 = dx2.contiguous()
+        s = [rt.grad_slot(unit, j) for j in range(12)]
+        # MLP
+        dm = F_.dropout(None, dx2, p, rt.seed, model.site_mlp(i))
+        F_.linear_wgrad(dm, g, s[10][0], s[11][0], s[10][1])
+        dg = torch.mm(dm, w2)
+        df = F_.gelu_bwd(dg, f, s[9][0], s[9][1])
+        F_.linear_wgrad(df, h2, s[8][0], None, s[8][1])
+        dh2 = torch.mm(df, w1)
+        dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False)
+        # attention
+        F_.linear_wgrad(dx1, o, s[4][0], s[5][0], s[4][1])
+        do = torch.mm(dx1, wo)
+        dqkv = torch.empty_like(qkv)
+        F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse,
+                    dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
+                    1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
+        F_.linear_wgrad(dqkv, h1, s[2][0], s[3][0], s[2][1])
+        dh1 = torch.mm(dqkv, win)
+        dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False)
+        rt.grads_ready(unit)
+        rt.release_backward(unit)
+        return dx, None, None
+
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, model, targets, return_logits):
+        rt = model.rt
+        lnw, lnb = rt.acquire(model.unit_head)
+        wte = rt.acquire_tied(model.unit_embed)[0]
+        _, h, mean, rstd = F_.norm_fwd(x, None, lnw, lnb, LN_EPS, False)
+        logits = F_.linear_fwd(h, wte)
+        if targets is None:
+            rt.release_forward(model.unit_head)
+            ctx.mark_non_differentiable(logits)
+            ctx.no_loss = True
+            return logits, logits.new_zeros(())
+        kept = logits.clone() if return_logits else None
+        tg = targets.reshape(-1)
+        loss_rows = F_.xent_fwd_bwd_(logits, tg, -1)
+        count = (tg != -1).sum().clamp(min=1).to(torch.float32)
+        loss = loss_rows.sum() / count
+        rt.release_forward(model.unit_head)
+        ctx.model, ctx.no_loss = model, False
+        ctx.saved = (x, h, mean, rstd, logits, count)
+        out_logits = kept if kept is not None else logits.new_empty(0)
+        ctx.mark_non_differentiable(out_logits)
+        return out_logits, loss
+
+    @staticmethod
+    def backward(ctx, dlogits_unused, dloss):
+        if ctx.no_loss:
+            return None, None, None, None
+        model = ctx.model
+        rt = model.rt
+        (x, h, mean, rstd, dl, count) = ctx.saved
+        ctx.saved = None
+        lnw, lnb = rt.acquire_backward(model.unit_head)
+        wte = rt.acquire_tied(model.unit_embed)[0]
+        g = (dloss.to(torch.float32) / count)
+        dw, acc_w = rt.grad_slot(model.unit_embed, 0)            # tied lm_head / wte
+        hs = (h * g).to(h.dtype)
+        F_.linear_wgrad(dl, hs, dw, None, acc_w)
+        dh = (torch.mm(dl, wte) * g).to(h.dtype)
+        gw, acc = rt.grad_slot(model.unit_head, 0)
+        gb, _ = rt.grad_slot(model.unit_head, 1)
+        dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False)
+        rt.grads_ready(model.unit_head)
+        rt.release_backward(model.unit_head)
+        return dx, None, None, None
+
+
+# ============================================================================ module
+class TinyGPT(nn.Module):
+    """Reference-compatible TinyGPT (train_harness.py:36-105) on fused MI355X kernels."""
+
+    def __init__(self, cfg: ModelConfig):
+        super().__init__()
+        self.cfg = cfg
+        d = cfg.n_embd
+        self.transformer = nn.ModuleDict({
+            "wte": nn.Embedding(cfg.vocab_size, d),
+            "wpe": nn.Embedding(cfg.block_size, d),
+            "drop": nn.Dropout(cfg.dropout),
+            "h": nn.ModuleList([TinyGPTBlock(d, cfg.n_head, cfg.dropout) for _ in range(cfg.n_layer)]),
+            "ln_f": nn.LayerNorm(d),
+        })
+        self.lm_head = nn.Linear(d, cfg.vocab_size, bias=False)
+        self.transformer["wte"].weight = self.lm_head.weight       # weight tying (train_harness.py:61)
+        self.apply(self._init_weights)
+        self.rt = EAGER
+        self.drop_p = cfg.dropout
+        self._build_units()
+
+    @staticmethod
+    def _init_weights(module):
+        if isinstance(module, nn.Linear):
+            nn.init.normal_(module.weight, mean=0.0, std=0.02)
+            if module.bias is not None:
+                nn.init.zeros_(module.bias)
+        elif isinstance(module, nn.Embedding):
+            nn.init.normal_(module.weight, mean=0.0, std=0.02)
+        elif isinstance(module, nn.LayerNorm):
+            nn.init.zeros_(module.bias)
+            nn.init.ones_(module.weight)
+
+    def _build_units(self):
+        t = self.transformer
+        self.unit_embed = Unit("embed", [("transformer.wte.weight", t["wte"].weight),
+                                         ("transformer.wpe.weight", t["wpe"].weight)], 0)
+        self.unit_blocks = [Unit(f"h.{i}", [(f"transformer.h.{i}.{n}", p) for n, p in blk.param_list()], i + 1)
+                            for i, blk in enumerate(t["h"])]
+        self.unit_head = Unit("head", [("transformer.ln_f.weight", t["ln_f"].weight),
+                                       ("transformer.ln_f.bias", t["ln_f"].bias)], len(self.unit_blocks) + 1)
+
+    def units(self):
+        """Units in forward order (the engines reverse it for backward-ordered buckets)."""
+        return [self.unit_embed] + self.unit_blocks + [self.unit_head]
+
+    # dropout sites: 0 = embedding, 1 + 2i = attention probs of block i, 2 + 2i = MLP output
+    site_embed = 0
+
+    @staticmethod
+    def site_attn(i):
+        return 1 + 2 * i
+
+    @staticmethod
+    def site_mlp(i):
+        return 2 + 2 * i
+
+    def num_params(self):
+        return sum(p.numel() for p in self.parameters())
+
+    def forward(self, idx, targets=None, return_logits=False):
+        B, T = idx.shape
+        assert T <= self.cfg.block_size, f"Sequence {T} exceeds block size {self.cfg.block_size}"
+        self._cur_bt = (B, T)
+        if not self.training:
+            self.drop_p = 0.0
+        else:
+            self.drop_p = self.cfg.dropout
+        if self.drop_p > 0 and self.rt.seed is None:
+            raise RuntimeError("dropout needs a StepSeed on the runtime (engine.attach or rt.seed = ...)")
+        anchor = torch.empty((), requires_grad=True)    # graph entry (CPU scalar, never updated)
+        x = _EmbedFn.apply(anchor, idx, self)
+        for i in range(len(self.unit_blocks)):
+            x = _BlockFn.apply(x, self, i)
+        logits, loss = _HeadFn.apply(x, self, targets, return_logits)
+        if targets is None:
+            return logits.view(B, T, -1), None
+        return (logits.view(B, T, -1) if return_logits else None), loss

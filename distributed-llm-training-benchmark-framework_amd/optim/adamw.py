@@ -1,0 +1,85 @@
+"""Fused AdamW over a flat fp32 owner space.
+
+Replaces ``torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)``
+(train_harness.py:328-329) and DeepSpeed's FusedAdam (``"optimizer": {"type": "AdamW"}`` in
+configs/deepspeed/zero{2,3}.json).  The rank's optimizer state — fp32 master weights, exp_avg,
+exp_avg_sq — lives in three flat tensors; one HIP launch (csrc/adamw.hip) reads master/m/v/grad
+once and writes master/m/v plus the bf16 compute copy of every parameter straight into its
+destination (the replicated flat parameter buffer, or this rank's parameter shard).
+"""
+import math
+from typing import List, Sequence, Tuple
+
+import torch
+
+from ..ops import ref
+from ..ops._ext import ext
+
+
+class FlatAdamW:
+    def __init__(self, master: torch.Tensor, segments: Sequence[Tuple[int, int, torch.Tensor]],
+                 lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
+        """``segments``: (owner_start, length, dst) with ``dst`` a contiguous 1-D view of length
+        ``length`` receiving the compute-dtype copy of ``master[owner_start:owner_start+length]``."""
+        assert master.dtype == torch.float32 and master.dim() == 1
+        self.master = master
+        self.exp_avg = torch.zeros_like(master)
+        self.exp_avg_sq = torch.zeros_like(master)
+        self.segments = list(segments)
+        self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
+        self.step_count = 0
+        self._tables = None
+        if master.is_cuda:
+            self._build_tables()
+
+    def _build_tables(self):
+        chunk = ext().adamw_chunk()
+        blk_seg: List[int] = []
+        blk_start: List[int] = []
+        so, sl, sd = [], [], []
+        for i, (ostart, length, dst) in enumerate(self.segments):
+            assert dst.is_contiguous() and dst.numel() == length
+            assert length % 4 == 0 and ostart % 4 == 0 and dst.data_ptr() % 8 == 0, "AdamW segments must be 4-aligned"
+            so.append(ostart)
+            sl.append(length)
+            sd.append(dst.data_ptr())
+            for s in range(ostart, ostart + length, chunk):
+                blk_seg.append(i)
+                blk_start.append(s)
+        dev = self.master.device
+        self._tables = (torch.tensor(blk_seg, dtype=torch.int32, device=dev),
+                        torch.tensor(blk_start, dtype=torch.int64, device=dev),
+                        torch.tensor(so, dtype=torch.int64, device=dev),
+                        torch.tensor(sl, dtype=torch.int64, device=dev),
+                        torch.tensor(sd, dtype=torch.int64, device=dev))
+
+    @torch.no_grad()
+    def step(self, grad: torch.Tensor, lr: float, gscale: torch.Tensor = None):
+        assert grad.numel() == self.master.numel()
+        self.step_count += 1
+        b1, b2 = self.betas
+        if self.master.is_cuda:
+            ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, *self._tables, gscale,
+                        lr, b1, b2, self.eps, self.weight_decay, self.step_count)
+            return
+        ref.adamw_flat(self.master, self.exp_avg, self.exp_avg_sq, grad, lr, b1, b2, self.eps,
+                       self.weight_decay, self.step_count, gscale)
+        for ostart, length, dst in self.segments:
+            dst.copy_(self.master[ostart:ostart + length])
+
+    def state_dict(self):
+        return {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,
+                "exp_avg_sq": self.exp_avg_sq, "lr": self.lr, "betas": self.betas, "eps": self.eps,
+                "weight_decay": self.weight_decay}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.master.copy_(sd["master"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        for ostart, length, dst in self.segments:
+            dst.copy_(self.master[ostart:ostart + length])
+
+    @property
+    def state_bytes(self) -> int:
+        return 3 * self.master.numel() * 4

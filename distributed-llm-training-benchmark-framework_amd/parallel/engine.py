@@ -1,0 +1,191 @@
+"""Common training-engine machinery shared by the DDP / ZeRO / FSDP engines.
+
+An engine owns the model's parameter storage (flat bf16 buffers), its gradient storage, the fused
+optimizer over the rank's fp32 owner space and the collectives.  Its public API mirrors what the
+reference harness drives (DeepSpeed's engine interface, train_harness.py:364-368, and the AMP
+loop, :370-382):
+
+    loss = engine(batch, targets)[1]       # forward (one micro-batch)
+    engine.backward(loss)                  # backward + gradient collectives
+    engine.step()                          # optimizer step at accumulation boundaries
+
+Micro-step bookkeeping: ``grad_accum`` micro-steps form one accumulation window; the last one is
+the *boundary* where the optimizer runs (with gradient clipping and the LR schedule when
+configured).  Gradients are averaged over ranks and micro-steps by folding ``1/(world*accum)``
+(and the clipping coefficient) into the optimizer's device-side gradient scale — no extra pass
+over the gradients and no host synchronisation.
+"""
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops._ext import ext
+from ..ops.rng import StepSeed
+from ..optim.sched import build_scheduler
+from .runtime import ParamRuntime, Unit
+
+
+@dataclass
+class EngineConfig:
+    strategy: str = "ddp"
+    lr: float = 1e-4
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.01
+    grad_accum: int = 1
+    grad_clip: float = 0.0
+    scheduler: Optional[dict] = None          # DeepSpeed-style {"type": "WarmupLR", "params": {...}}
+    compute_dtype: torch.dtype = torch.bfloat16
+    bucket_mb: float = 64.0                   # gradient bucket cap (xGMI-tuned default)
+    seed: int = 42
+    # sharded engines
+    reshard_after_forward: bool = True
+    prefetch: int = 1                         # units gathered ahead (forward and backward)
+    persistence_threshold: int = 0            # ZeRO-3: params below this numel stay replicated
+    max_live_parameters: int = 0              # ZeRO-3: keep gathered params if the model fits
+    max_reuse_distance: int = 0
+    wrap: str = "block"                       # FSDP: "block" (per transformer block) | "root"
+    zero_stage: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+class Engine(ParamRuntime):
+    name = "engine"
+
+    def __init__(self, model, cfg: EngineConfig, device, group=None):
+        super().__init__()
+        self.model = model
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+        else:
+            self.world, self.rank = 1, 0
+        self.accum = max(1, int(cfg.grad_accum))
+        self.compute_dtype = cfg.compute_dtype if self.device.type == "cuda" else torch.float32
+        self.seed = StepSeed(cfg.seed, self.rank, self.device)
+        self.sched = build_scheduler(cfg.scheduler, cfg.lr)
+        self.micro = 0
+        self.opt_steps = 0
+        self._is_boundary = self.accum == 1
+        self._window_pos = 0
+        self._written = {}
+        self._works = []
+        self.last_lr = None
+        self.grad_norm = None
+        self._norm_sq = torch.zeros(1, device=self.device, dtype=torch.float32)
+        self._gscale = torch.ones(1, device=self.device, dtype=torch.float32)
+        self.comm_bytes_per_step = 0
+        model.rt = self
+        self._setup()
+
+    # ------------------------------------------------------------------ subclass hooks
+    def _setup(self):
+        raise NotImplementedError
+
+    def _on_begin_micro(self):
+        pass
+
+    def _finish_backward(self):
+        pass
+
+    def _optimizer_step(self, lr: float):
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------ public API
+    def __call__(self, idx, targets=None):
+        return None, self.forward(idx, targets)
+
+    def forward(self, idx, targets=None):
+        self._begin_micro()
+        _, loss = self.model(idx, targets)
+        return loss
+
+    def backward(self, loss):
+        loss.backward()
+        self._finish_backward()
+
+    def step(self):
+        if self._is_boundary:
+            lr = self.sched(self.opt_steps)
+            self.last_lr = lr
+            self._optimizer_step(lr)
+            self.opt_steps += 1
+        self.micro += 1
+
+    def train(self, mode=True):
+        self.model.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def zero_grad(self, set_to_none=True):   # grads are overwritten at window start; kept for API parity
+        pass
+
+    @property
+    def is_boundary(self):
+        return self._is_boundary
+
+    # ------------------------------------------------------------------ micro-step bookkeeping
+    def _begin_micro(self):
+        self.seed.next()
+        self._window_pos = self.micro % self.accum
+        self._is_boundary = self._window_pos == self.accum - 1
+        if self._window_pos == 0:
+            self._written.clear()
+        self._on_begin_micro()
+
+    def _mark(self, unit: Unit, i: int) -> bool:
+        """Returns True when the slot already holds data of this accumulation window."""
+        key = (id(unit), i)
+        acc = self._written.get(key, False)
+        self._written[key] = True
+        return acc
+
+    # ------------------------------------------------------------------ helpers
+    def _wait_works(self):
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+
+    def _sumsq_into(self, t: torch.Tensor, out: torch.Tensor):
+        if t.is_cuda:
+            ext().sumsq_(t, out)
+        else:
+            out += t.float().pow(2).sum()
+
+    def _clip_coef(self, grads, extra_scale: float, sharded: bool):
+        """Device gradient scale = extra_scale * min(1, clip / ||extra_scale * g||).  Also records
+        the global gradient norm in ``self.grad_norm`` (device tensor)."""
+        want_norm = self.cfg.grad_clip > 0 or self.cfg.extra.get("track_grad_norm", False)
+        if not want_norm:
+            self._gscale.fill_(extra_scale)
+            return self._gscale
+        self._norm_sq.zero_()
+        for g in grads:
+            self._sumsq_into(g, self._norm_sq)
+        if sharded and self.world > 1:
+            dist.all_reduce(self._norm_sq, group=self.group)
+        if self.device.type == "cuda":
+            if self.grad_norm is None:
+                self.grad_norm = torch.zeros(1, device=self.device)
+            ext().clip_coef(self._norm_sq, float(self.cfg.grad_clip), self._gscale, self.grad_norm, extra_scale)
+        else:
+            nrm = self._norm_sq.sqrt() * extra_scale
+            c = torch.clamp(self.cfg.grad_clip / (nrm + 1e-6), max=1.0) if self.cfg.grad_clip > 0 else torch.ones_like(nrm)
+            self._gscale.copy_(c * extra_scale)
+            self.grad_norm = nrm
+        return self._gscale
+
+    # ------------------------------------------------------------------ introspection
+    def memory_report(self) -> dict:
+        return {}
+
+    def full_state_dict(self) -> dict:
+        """Gather a full fp32 state dict (master weights) on every rank."""
+        raise NotImplementedError

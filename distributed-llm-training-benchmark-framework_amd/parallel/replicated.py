@@ -1,0 +1,197 @@
+"""Replicated-parameter engines: DDP and ZeRO-1/2.
+
+Reference strategies (train_harness.py:210-223 torch DDP; :240-271 + configs/deepspeed/zero2.json
+DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
+
+* Parameters: ONE flat bf16 buffer in backward order (head, block L-1 ... block 0, embedding), every
+  ``nn.Parameter`` a view into it.  Gradients: a flat bf16 buffer with the same layout, written in
+  place by the fused block backward (no autograd hooks, no bucket copies).
+* Buckets: consecutive units grouped up to ``bucket_mb`` (xGMI-tuned default 64 MiB).  When the
+  last unit of a bucket finishes its backward the engine launches the bucket's collective
+  immediately (async, on the process group's stream) so communication overlaps the remaining
+  backward.
+* DDP (``zero_stage=0``): SUM all-reduce per bucket; the 1/world average is folded into the fused
+  AdamW's gradient scale.  fp32 master / Adam moments for the whole model on every rank.
+* ZeRO-2: reduce-scatter per bucket, every micro-step, into this rank's chunk; chunks accumulate
+  in an fp32 owner buffer across the ``grad_accum`` window; at the boundary: global grad-norm
+  (one float all-reduce), clipping coefficient on device, fused AdamW on the owner shard writing
+  the bf16 chunk in place, then an in-place all-gather per bucket re-replicates the parameters.
+* ZeRO-1: like ZeRO-2 but gradients accumulate unsharded and are reduce-scattered at the boundary.
+"""
+import torch
+import torch.distributed as dist
+
+from ..ops._ext import ext
+from ..optim.adamw import FlatAdamW
+from .engine import Engine
+from .flat import ALIGN, owner_segments, plan_layout
+
+
+class ReplicatedEngine(Engine):
+    name = "ddp"
+
+    def _setup(self):
+        cfg, model = self.cfg, self.model
+        self.stage = int(cfg.zero_stage)
+        units = list(reversed(model.units()))
+        elem = torch.tensor([], dtype=self.compute_dtype).element_size()
+        bucket_elems = int(cfg.bucket_mb * (1 << 20) / elem) if cfg.bucket_mb > 0 else 0
+        ds_cap = cfg.extra.get("reduce_bucket_elems")
+        if ds_cap:
+            bucket_elems = min(bucket_elems, int(ds_cap)) if bucket_elems else int(ds_cap)
+        shard = self.stage >= 1
+        self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard)
+        dev, dt = self.device, self.compute_dtype
+        master_full = torch.zeros(L.total, dtype=torch.float32, device=dev)
+        for s in L.slots.values():
+            p = s.unit.params[s.index]
+            master_full[s.offset:s.offset + s.numel] = p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
+        self.flat_param = master_full.to(dt)
+        self.flat_grad = torch.zeros(L.total, dtype=dt, device=dev)
+        for s in L.slots.values():
+            p = s.unit.params[s.index]
+            p.data = self.flat_param[s.offset:s.offset + s.numel].view(s.shape)
+            p.grad = None
+        if shard:
+            segs = owner_segments(L, self.rank)
+            master = torch.empty(L.owner_numel, dtype=torch.float32, device=dev)
+            opt_segs = []
+            for ostart, ln, fstart in segs:
+                master[ostart:ostart + ln] = master_full[fstart:fstart + ln]
+                opt_segs.append((ostart, ln, self.flat_param[fstart:fstart + ln]))
+            self.rs_out = torch.zeros(L.owner_numel, dtype=dt, device=dev) if self.world > 1 else None
+            self.acc = torch.zeros(L.owner_numel, dtype=torch.float32, device=dev) if self.accum > 1 else None
+        else:
+            master = master_full
+            opt_segs = [(0, L.total, self.flat_param)]
+            self.rs_out = self.acc = None
+        del master_full
+        self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
+        self._pending = [len(b.units) for b in L.buckets]
+        self._bucket_of = L.unit_bucket
+        self._launched = [False] * len(L.buckets)
+        nbytes = L.total * elem
+        if self.world > 1:
+            ring = 2 * (self.world - 1) / self.world
+            self.comm_bytes_per_step = int(nbytes * (ring if self.stage == 0 else ring / 2))
+
+    # ------------------------------------------------------------------ runtime interface
+    def acquire(self, unit):
+        return [p.detach() for p in unit.params]
+
+    acquire_backward = acquire
+
+    def grad_slot(self, unit, i):
+        s = self.layout.slot(unit, i)
+        return self.flat_grad[s.offset:s.offset + s.numel].view(s.shape), self._mark(unit, i)
+
+    def _reduce_now(self) -> bool:
+        if self.world == 1:
+            return False
+        if self.stage == 2:
+            return True
+        return self._is_boundary
+
+    def grads_ready(self, unit):
+        b = self._bucket_of.get(id(unit))
+        if b is None:
+            return
+        self._pending[b] -= 1
+        if self._pending[b] == 0 and self._reduce_now():
+            self._launch(b)
+
+    def _launch(self, b):
+        bk = self.layout.buckets[b]
+        g = self.flat_grad[bk.start:bk.end]
+        if self.stage == 0:
+            w = dist.all_reduce(g, group=self.group, async_op=True)
+        else:
+            out = self.rs_out[bk.owner_start:bk.owner_start + bk.chunk]
+            w = dist.reduce_scatter_tensor(out, g, group=self.group, async_op=True)
+        self._works.append(w)
+        self._launched[b] = True
+
+    # ------------------------------------------------------------------ step lifecycle
+    def _on_begin_micro(self):
+        if self.stage == 2:
+            self._written.clear()         # the full gradient buffer is reduced every micro-step
+
+    def _finish_backward(self):
+        if self._reduce_now():
+            for b, done in enumerate(self._launched):   # units that never reported (unused params)
+                if not done:
+                    self._launch(b)
+        self._wait_works()
+        self._pending = [len(b.units) for b in self.layout.buckets]
+        self._launched = [False] * len(self.layout.buckets)
+        if self.stage == 2 and self.acc is not None:
+            src = self.rs_out if self.world > 1 else self.flat_grad
+            first = self._window_pos == 0
+            if self.acc.is_cuda:
+                ext().f32_from_bf16_(self.acc, src, not first)
+            elif first:
+                self.acc.copy_(src)
+            else:
+                self.acc += src
+
+    def _owner_grad(self):
+        if self.stage == 0:
+            return self.flat_grad
+        if self.acc is not None and self.stage == 2:
+            return self.acc
+        return self.rs_out if self.world > 1 else self.flat_grad
+
+    def _optimizer_step(self, lr):
+        # (ZeRO-1 reduce-scattered its window-accumulated gradients during the boundary backward)
+        g = self._owner_grad()
+        extra = 1.0 / (self.world * self.accum)
+        gscale = self._clip_coef([g], extra, sharded=self.stage >= 1)
+        self.opt.step(g, lr, gscale)
+        if self.stage >= 1 and self.world > 1:
+            for bk in self.layout.buckets:
+                full = self.flat_param[bk.start:bk.end]
+                mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
+                self._works.append(dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True))
+            self._wait_works()
+
+    # ------------------------------------------------------------------ introspection
+    def memory_report(self):
+        e = self.flat_param.element_size()
+        return {"param_bytes": self.flat_param.numel() * e, "grad_bytes": self.flat_grad.numel() * e,
+                "optimizer_bytes": self.opt.state_bytes,
+                "buckets": len(self.layout.buckets),
+                "bucket_mb": [round(b.numel * e / 2**20, 2) for b in self.layout.buckets]}
+
+    def full_state_dict(self):
+        out = {}
+        if self.stage >= 1 and self.world > 1:
+            full = torch.zeros(self.layout.total, dtype=torch.float32, device=self.device)
+            for ostart, ln, fstart in owner_segments(self.layout, self.rank):
+                full[fstart:fstart + ln] = self.opt.master[ostart:ostart + ln]
+            dist.all_reduce(full, group=self.group)
+        elif self.stage >= 1:
+            full = torch.zeros(self.layout.total, dtype=torch.float32, device=self.device)
+            for ostart, ln, fstart in owner_segments(self.layout, self.rank):
+                full[fstart:fstart + ln] = self.opt.master[ostart:ostart + ln]
+        else:
+            full = self.opt.master
+        for s in self.layout.slots.values():
+            out[s.unit.names[s.index]] = full[s.offset:s.offset + s.numel].view(s.shape).clone()
+        return out
+
+
+class DDPEngine(ReplicatedEngine):
+    name = "ddp"
+
+    def __init__(self, model, cfg, device, group=None):
+        cfg.zero_stage = 0
+        super().__init__(model, cfg, device, group)
+
+
+class Zero2Engine(ReplicatedEngine):
+    name = "zero2"
+
+    def __init__(self, model, cfg, device, group=None):
+        if cfg.zero_stage not in (1, 2):
+            cfg.zero_stage = 2
+        super().__init__(model, cfg, device, group)

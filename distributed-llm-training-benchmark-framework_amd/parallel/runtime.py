@@ -1,0 +1,84 @@
+"""Parameter runtime interface between the fused model Functions and a parallelism engine.
+
+The models in :mod:`dltb.models` are chains of fused autograd Functions (embedding, one Function
+per transformer block, head+loss).  Each Function works on one *unit* of parameters and talks to
+the runtime instead of to ``nn.Parameter.grad``:
+
+    forward : params = rt.acquire(unit)            ... compute ...   rt.release_forward(unit)
+    backward: params = rt.acquire_backward(unit)   (re-gathers / prefetches under FSDP, ZeRO-3)
+              slot, acc = rt.grad_slot(unit, i)    (flat-buffer gradient view + overwrite/accumulate)
+              ... GEMMs write dW straight into the slots ...
+              rt.grads_ready(unit)                 (DDP: bucket all-reduce; ZeRO/FSDP: reduce-scatter)
+              rt.release_backward(unit)
+
+This is the MI355X-native replacement for the reference's reliance on autograd hooks inside
+torch DDP's C++ Reducer / FSDP / DeepSpeed (train_harness.py:207-275): the engines know exactly
+when a unit's gradients are complete, launch their RCCL collective right then on the process
+group's stream, and never copy gradients between buffers.
+"""
+from typing import List, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+
+class Unit:
+    """An ordered group of parameters gathered / reduced together."""
+
+    def __init__(self, name: str, params: Sequence[Tuple[str, nn.Parameter]], index: int = 0):
+        self.name = name
+        self.names = [n for n, _ in params]
+        self.params = [p for _, p in params]
+        self.index = index
+        self.shapes = [tuple(p.shape) for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+
+    @property
+    def numel(self) -> int:
+        return sum(self.numels)
+
+    def __repr__(self):
+        return f"Unit({self.name}, {len(self.params)} params, {self.numel} elems)"
+
+
+class ParamRuntime:
+    """Interface + the eager default used when no engine is attached (CPU tests, oracles).
+
+    Eager semantics mirror autograd: gradients accumulate into ``param.grad`` (allocated on the first
+    write), so a model without an engine behaves like a plain nn.Module under ``loss.backward()``.
+    """
+
+    def __init__(self):
+        self.seed = None          # dltb.ops.rng.StepSeed
+        self.compute_dtype = None
+
+    # forward
+    def acquire(self, unit: Unit) -> List[torch.Tensor]:
+        return [p.detach() for p in unit.params]
+
+    def release_forward(self, unit: Unit):
+        pass
+
+    def acquire_tied(self, unit: Unit) -> List[torch.Tensor]:
+        """Parameters of another unit used by a tied consumer (the head reads wte)."""
+        return self.acquire(unit)
+
+    # backward
+    def acquire_backward(self, unit: Unit) -> List[torch.Tensor]:
+        return [p.detach() for p in unit.params]
+
+    def grad_slot(self, unit: Unit, i: int) -> Tuple[torch.Tensor, bool]:
+        p = unit.params[i]
+        if p.grad is None:
+            p.grad = torch.empty_like(p)
+            return p.grad, False
+        return p.grad, True
+
+    def grads_ready(self, unit: Unit):
+        pass
+
+    def release_backward(self, unit: Unit):
+        pass
+
+
+EAGER = ParamRuntime()

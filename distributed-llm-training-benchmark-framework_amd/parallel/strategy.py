@@ -1,0 +1,123 @@
+"""Strategy dispatcher: the MI355X-native replacement of the reference's ``wrap_model``
+(train_harness.py:207-275).
+
+``--strategy ddp | fsdp | zero2 | zero3`` selects an engine; the DeepSpeed JSON
+(``--deepspeed-config``) and FSDP YAML (``--fsdp-config``) are read by our own schema readers (no
+DeepSpeed dependency; the reference never reads its FSDP YAML at all).
+
+Step semantics (``--accum-semantics``):
+  reference (default) — what the reference actually runs: DDP/FSDP step the optimizer every
+      micro-batch (``--grad-accum`` ignored, no clipping, constant lr 1e-4, wd 0.01,
+      train_harness.py:328-382); ZeRO-2/3 accumulate ``grad_accum`` micro-batches, clip the global
+      grad norm to 1.0 and use WarmupLR (zero2.json).
+  uniform — every strategy gets the ZeRO semantics (accumulation + clipping + schedule).
+"""
+import json
+import math
+import os
+from typing import Optional
+
+import torch
+
+from .engine import EngineConfig
+from .replicated import DDPEngine, Zero2Engine
+from .sharded import FSDPEngine, Zero3Engine
+
+STRATEGIES = ("ddp", "fsdp", "zero2", "zero3")
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def default_config_path(strategy: str) -> Optional[str]:
+    if strategy in ("zero2", "zero3"):
+        return os.path.join(_ROOT, "configs", "deepspeed", f"{strategy}.json")
+    if strategy == "fsdp":
+        return os.path.join(_ROOT, "configs", "fsdp", "fsdp_config.yaml")
+    return None
+
+
+def _num(v, default=None):
+    if v is None or v == "auto":
+        return default
+    return float(v) if not isinstance(v, bool) else v
+
+
+def load_deepspeed_config(path: str) -> dict:
+    with open(path) as f:
+        return json.load(f)
+
+
+def load_fsdp_config(path: str) -> dict:
+    import yaml
+    with open(path) as f:
+        data = yaml.safe_load(f) or {}
+    return data.get("fsdp_config", data)
+
+
+def engine_config(strategy: str, grad_accum: int = 1, semantics: str = "reference",
+                  ds_config: Optional[dict] = None, fsdp_config: Optional[dict] = None,
+                  compute_dtype=torch.bfloat16, bucket_mb: float = 64.0, seed: int = 42,
+                  overrides: Optional[dict] = None) -> EngineConfig:
+    if strategy not in STRATEGIES:
+        raise ValueError(f"unknown strategy {strategy}")
+    cfg = EngineConfig(strategy=strategy, compute_dtype=compute_dtype, bucket_mb=bucket_mb, seed=seed)
+    ds = ds_config or {}
+    opt = (ds.get("optimizer") or {}).get("params", {})
+    zero_like = strategy in ("zero2", "zero3") or semantics == "uniform"
+    if zero_like:
+        cfg.lr = _num(opt.get("lr"), 1e-4)
+        cfg.betas = tuple(opt.get("betas", (0.9, 0.999)))
+        cfg.eps = _num(opt.get("eps"), 1e-8)
+        cfg.weight_decay = _num(opt.get("weight_decay"), 0.01)
+        cfg.grad_accum = max(1, int(grad_accum))
+        cfg.grad_clip = _num(ds.get("gradient_clipping"), 1.0 if not ds else 0.0)
+        sched = ds.get("scheduler")
+        if sched is None and not ds:
+            sched = {"type": "WarmupLR", "params": {"warmup_min_lr": 0, "warmup_max_lr": cfg.lr,
+                                                    "warmup_num_steps": 5}}
+        cfg.scheduler = sched
+    else:   # reference DDP / FSDP: AdamW(lr=1e-4, wd=0.01) every micro-step
+        cfg.lr, cfg.weight_decay, cfg.grad_accum, cfg.grad_clip, cfg.scheduler = 1e-4, 0.01, 1, 0.0, None
+    z = ds.get("zero_optimization", {}) or {}
+    if strategy == "zero2":
+        cfg.zero_stage = int(z.get("stage", 2)) if int(z.get("stage", 2)) in (1, 2) else 2
+        rb = _num(z.get("reduce_bucket_size"))
+        if rb:
+            cfg.extra["reduce_bucket_elems"] = int(rb)
+    if strategy == "zero3":
+        cfg.zero_stage = 3
+        cfg.persistence_threshold = int(_num(z.get("stage3_param_persistence_threshold"), 1e5))
+        cfg.max_live_parameters = int(_num(z.get("stage3_max_live_parameters"), 1e9))
+        cfg.max_reuse_distance = int(_num(z.get("stage3_max_reuse_distance"), 1e9))
+        cfg.prefetch = 1 if _num(z.get("stage3_prefetch_bucket_size"), 5e8) > 0 else 0
+        cfg.reshard_after_forward = True
+        cfg.wrap = "unit"
+    if strategy == "fsdp":
+        fc = fsdp_config or {}
+        ss = str(fc.get("sharding_strategy", "full_shard")).lower()
+        cfg.reshard_after_forward = ss != "shard_grad_op"
+        if ss == "no_shard":
+            cfg.extra["no_shard"] = True
+        pol = str(fc.get("auto_wrap_policy", "transformer_block")).lower()
+        cfg.wrap = "root" if pol in ("size_based", "root", "none") else "block"
+        bp = str(fc.get("backward_prefetch", "backward_pre")).lower()
+        cfg.prefetch = 0 if bp in ("none", "false", "no") else 1
+        if fc.get("mixed_precision") is False and fc.get("param_dtype") == "float32":
+            cfg.compute_dtype = torch.float32
+    cfg.extra["semantics"] = semantics
+    for k, v in (overrides or {}).items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def make_engine(model, cfg: EngineConfig, device, group=None):
+    """Instantiate the engine for ``cfg.strategy`` (reference ``wrap_model`` equivalent)."""
+    s = cfg.strategy
+    if s == "ddp" or (s == "fsdp" and cfg.extra.get("no_shard")):
+        return DDPEngine(model, cfg, device, group)
+    if s == "zero2":
+        return Zero2Engine(model, cfg, device, group)
+    if s == "fsdp":
+        return FSDPEngine(model, cfg, device, group)
+    if s == "zero3":
+        return Zero3Engine(model, cfg, device, group)
+    raise ValueError(s)

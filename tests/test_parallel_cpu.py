@@ -1,0 +1,154 @@
+"""Engine correctness on CPU (gloo "fake cluster").
+
+* single process: every engine == stock torch training (oracle model + torch.optim.AdamW) under
+  the reference semantics;
+* world_size 2: every strategy (DDP, FSDP block/root wrap, ZeRO-2, ZeRO-3) reproduces the
+  single-process run on the concatenated global batch, with gradient accumulation for ZeRO.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dltb
+from dltb.models import get_model_config
+from dltb.models.oracle import OracleTinyGPT
+from dltb.models.tinygpt import TinyGPT
+from dltb.parallel import engine_config, make_engine
+
+T = 16
+STEPS = 4
+
+
+def _close(a, b, name, atol):
+    """The key part of in_proj_bias has an exactly-zero true gradient (softmax is invariant to a
+    per-row constant); Adam turns its rounding noise into +-lr steps, so it is not compared."""
+    if name.endswith("attn.in_proj_bias"):
+        d = a.numel() // 3
+        a = torch.cat([a[:d], a[2 * d:]])
+        b = torch.cat([b[:d], b[2 * d:]])
+    return torch.allclose(a, b, atol=atol)
+
+
+def _model():
+    torch.manual_seed(0)
+    return TinyGPT(get_model_config("tiny", T, dropout=0.0))
+
+
+def _batches(n_steps, global_batch):
+    g = torch.Generator().manual_seed(123)
+    return [torch.randint(0, 128, (global_batch, T), generator=g) for _ in range(n_steps)]
+
+
+def _cfg(strategy, accum, semantics="reference", **kw):
+    ds = None
+    if strategy in ("zero2", "zero3"):
+        ds = {"gradient_clipping": 1.0, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "weight_decay": 0.01}},
+              "scheduler": {"type": "WarmupLR", "params": {"warmup_min_lr": 0, "warmup_max_lr": 1e-3, "warmup_num_steps": 3}},
+              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 2000,
+                                    "stage3_param_persistence_threshold": 300,
+                                    "stage3_max_live_parameters": kw.pop("max_live", 1e9),
+                                    "stage3_max_reuse_distance": 1e9}}
+    fc = kw.pop("fsdp", None)
+    c = engine_config(strategy, accum, semantics, ds, fc, bucket_mb=kw.pop("bucket_mb", 0.01))
+    c.lr = 1e-3 if strategy in ("ddp", "fsdp") and semantics == "reference" else c.lr
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def _train(strategy, batches, rank, world, accum, **kw):
+    model = _model()
+    eng = make_engine(model, _cfg(strategy, accum, **kw), "cpu")
+    eng.train()
+    for b in batches:
+        per = b.shape[0] // world
+        mb = b[rank * per:(rank + 1) * per]
+        micro = mb.shape[0] // accum
+        for a in range(accum):
+            x = mb[a * micro:(a + 1) * micro]
+            loss = eng(x, x)[1]
+            eng.backward(loss)
+            eng.step()
+    return eng.full_state_dict()
+
+
+def test_single_process_ddp_matches_torch_adamw():
+    batches = _batches(STEPS, 2)
+    sd = _train("ddp", batches, 0, 1, 1)
+    torch.manual_seed(0)
+    ref_model = _model()
+    oracle = OracleTinyGPT(ref_model.cfg)
+    oracle.load_state_dict(ref_model.state_dict())
+    opt = torch.optim.AdamW(oracle.parameters(), lr=1e-3, weight_decay=0.01)
+    for b in batches:
+        _, loss = oracle(b, b)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+    for n, p in oracle.named_parameters():
+        assert _close(sd[n], p.detach(), n, 2e-5), n
+
+
+@pytest.mark.parametrize("strategy,kw", [
+    ("ddp", {}), ("zero2", {}), ("zero3", {}), ("zero3", {"max_live": 0}), ("fsdp", {}),
+    ("fsdp", {"fsdp": {"auto_wrap_policy": "size_based"}}),
+    ("fsdp", {"fsdp": {"sharding_strategy": "shard_grad_op"}}),
+])
+def test_single_process_engines_agree(strategy, kw):
+    """Every engine at world_size 1 trains identically to DDP under the same semantics."""
+    batches = _batches(STEPS, 2)
+    accum = 2 if strategy.startswith("zero") else 1
+    base = _train("ddp" if not strategy.startswith("zero") else "zero2", batches, 0, 1, accum)
+    got = _train(strategy, batches, 0, 1, accum, **dict(kw))
+    for n in base:
+        assert _close(got[n], base[n], n, 1e-6), (strategy, n)
+
+
+# ---------------------------------------------------------------- multi-process (gloo)
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, strategy, accum, kw, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        sd = _train(strategy, _batches(STEPS, 4), rank, world, accum, **kw)
+        if rank == 0:
+            torch.save(sd, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("strategy,accum,kw", [
+    ("ddp", 1, {}),
+    ("ddp", 2, {"semantics": "uniform"}),
+    ("zero2", 2, {}),
+    ("zero3", 2, {}),
+    ("zero3", 1, {"max_live": 0}),
+    ("fsdp", 1, {}),
+    ("fsdp", 1, {"fsdp": {"auto_wrap_policy": "size_based"}}),
+])
+def test_world2_matches_single_process(strategy, accum, kw):
+    world = 2
+    sem = kw.pop("semantics", "reference")
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "sd.pt")
+        mp.spawn(_worker, args=(world, _free_port(), strategy, accum, dict(kw, semantics=sem) if sem != "reference" else kw, out),
+                 nprocs=world, join=True)
+        got = torch.load(out, weights_only=True)
+    # single process on the concatenated batch: same global batch per micro-step
+    ref = _train(strategy, _batches(STEPS, 4), 0, 1, accum, **(dict(kw, semantics=sem) if sem != "reference" else kw))
+    for n in ref:
+        assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
