@@ -76,15 +76,36 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// sum P partial rows of [P][k] -> bf16 out (overwrite / accumulate); 16 column quads x 16 row
+// phases per 256-thread block, float4 loads.
 __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ part, int P,
                                                        int k, bf16_t* __restrict__ out,
                                                        int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= k) return;
-  float a = 0.f;
-  for (int p = 0; p < P; ++p) a += part[(size_t)p * k + c];
-  if (accumulate) a += bf2f(out[c]);
-  out[c] = f2bf(a);
+  __shared__ float red[16][65];
+  const int cq = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + cq * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < k) {
+    for (int p = ph; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(part + (size_t)p * k + c0);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[ph][cq * 4 + 0] = a.x;
+  red[ph][cq * 4 + 1] = a.y;
+  red[ph][cq * 4 + 2] = a.z;
+  red[ph][cq * 4 + 3] = a.w;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < k) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+      if (accumulate) t += bf2f(out[c]);
+      out[c] = f2bf(t);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------- dropout
@@ -253,7 +274,7 @@ void dltb_gelu_bwd(const void* dg, const void* f, void* df, float* part, void* d
   hipLaunchKernelGGL(colsum_kernel<true>, grid, dim3(256), 0, st, (const bf16_t*)dg,
                      (const bf16_t*)f, (bf16_t*)df, part, N, k, rps);
   if (db)
-    hipLaunchKernelGGL(colreduce_kernel, dim3(cdiv(k, 256)), dim3(256), 0, st, part, P, k,
+    hipLaunchKernelGGL(colreduce_kernel, dim3(cdiv(k, 64)), dim3(256), 0, st, part, P, k,
                        (bf16_t*)db, accumulate);
 }
 
@@ -264,7 +285,7 @@ void dltb_colsum(const void* src, float* part, void* out, int accumulate, int N,
   dim3 grid(cdiv(k, 512), P);
   hipLaunchKernelGGL(colsum_kernel<false>, grid, dim3(256), 0, st, (const bf16_t*)src, nullptr,
                      nullptr, part, N, k, rps);
-  hipLaunchKernelGGL(colreduce_kernel, dim3(cdiv(k, 256)), dim3(256), 0, st, part, P, k,
+  hipLaunchKernelGGL(colreduce_kernel, dim3(cdiv(k, 64)), dim3(256), 0, st, part, P, k,
                      (bf16_t*)out, accumulate);
 }
 

@@ -106,112 +106,139 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
   }
 }
 
-// dgamma/dbeta partials: part[blk][0][d] (dgamma), part[blk][1][d] (dbeta)
+// dx: one wave per row, 4 rows per block (full occupancy); dy and s are read twice, the second
+// pass hits L1/L2.
 template <int NV, bool RMS, bool HAS_RES_GRAD>
-__global__ __launch_bounds__(256) void norm_bwd_kernel(
+__global__ __launch_bounds__(256) void norm_bwd_dx_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N,
-    int d) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];   // [2][d]
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, int N, int d) {
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= N) return;
   const int nvec = d >> 3;
-  for (int i = threadIdx.x; i < 2 * d; i += blockDim.x) lds[i] = 0.f;
-  __syncthreads();
-  float gacc[NV][8], bacc[NV][8];
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { gacc[j][e] = 0.f; bacc[j][e] = 0.f; }
-  const int row0 = (blockIdx.x * kWaves + wid) * kRowsPerWave;
-  for (int rr = 0; rr < kRowsPerWave; ++rr) {
-    const int row = row0 + rr;
-    if (row >= N) break;
-    const size_t base = (size_t)row * d;
-    const float mean = RMS ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
-    float s1 = 0.f, s2 = 0.f;   // sum(w*dy), sum(w*dy*xhat)
-    // pass 1: row statistics + dgamma/dbeta partials
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int idx = j * 64 + lane;
-      if (idx < nvec) {
-        float dyv[8], xv[8], wv[8];
-        unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
-        unpack8(ld16<uint4>(s + base + idx * 8), xv);
-        unpack8(ld16<uint4>(w + idx * 8), wv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xh = (xv[e] - mean) * rstd;
-          const float g = dyv[e] * wv[e];
-          s1 += g;
-          s2 += g * xh;
-          gacc[j][e] += dyv[e] * xh;
-          bacc[j][e] += dyv[e];
-        }
-      }
-    }
-    s1 = RMS ? 0.f : wave_sum(s1) / (float)d;
-    s2 = wave_sum(s2) / (float)d;
-    // pass 2: dx (re-reads hit L1/L2)
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int idx = j * 64 + lane;
-      if (idx < nvec) {
-        float dyv[8], xv[8], wv[8], o[8];
-        unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
-        unpack8(ld16<uint4>(s + base + idx * 8), xv);
-        unpack8(ld16<uint4>(w + idx * 8), wv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xh = (xv[e] - mean) * rstd;
-          o[e] = rstd * (dyv[e] * wv[e] - s1 - xh * s2);
-        }
-        if (HAS_RES_GRAD) {
-          float rv[8];
-          unpack8(ld16<uint4>(dres + base + idx * 8), rv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] += rv[e];
-        }
-        *reinterpret_cast<uint4*>(dx + base + idx * 8) = pack8(o);
-      }
-    }
-  }
+  const size_t base = (size_t)row * d;
+  const float mean = RMS ? 0.f : mean_in[row];
+  const float rstd = rstd_in[row];
+  float s1 = 0.f, s2 = 0.f;   // sum(w*dy), sum(w*dy*xhat)
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int idx = j * 64 + lane;
     if (idx < nvec) {
+      float dyv[8], xv[8], wv[8];
+      unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
+      unpack8(ld16<uint4>(s + base + idx * 8), xv);
+      unpack8(ld16<uint4>(w + idx * 8), wv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        atomicAdd(&lds[idx * 8 + e], gacc[j][e]);
-        if (!RMS) atomicAdd(&lds[d + idx * 8 + e], bacc[j][e]);
+        const float g = dyv[e] * wv[e];
+        s1 += g;
+        s2 += g * (xv[e] - mean) * rstd;
       }
     }
   }
-  __syncthreads();
-  float* out = part + (size_t)blockIdx.x * 2 * d;
-  for (int i = threadIdx.x; i < 2 * d; i += blockDim.x) out[i] = lds[i];
+  s1 = RMS ? 0.f : wave_sum(s1) / (float)d;
+  s2 = wave_sum(s2) / (float)d;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int idx = j * 64 + lane;
+    if (idx < nvec) {
+      float dyv[8], xv[8], wv[8], o[8];
+      unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
+      unpack8(ld16<uint4>(s + base + idx * 8), xv);
+      unpack8(ld16<uint4>(w + idx * 8), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rstd * (dyv[e] * wv[e] - s1 - (xv[e] - mean) * rstd * s2);
+      if (HAS_RES_GRAD) {
+        float rv[8];
+        unpack8(ld16<uint4>(dres + base + idx * 8), rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += rv[e];
+      }
+      *reinterpret_cast<uint4*>(dx + base + idx * 8) = pack8(o);
+    }
+  }
 }
 
-// sum P partial rows of [P][2][d] -> bf16 gamma grad (and beta grad if gb != null)
+// dgamma / dbeta column partials: block (bx, by) covers columns [bx*512, +512) and rows
+// [by*rps, +rps); lane -> 8 columns, wave -> every 4th row.  part: [2][P][d]
+template <bool RMS>
+__global__ __launch_bounds__(256) void norm_dgamma_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, float* __restrict__ part, int N, int d, int rps) {
+  __shared__ __attribute__((aligned(16))) float red[2][4][512];
+  const int lane = threadIdx.x & 63, phase = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + lane * 8;
+  const int r0 = blockIdx.y * rps;
+  const int r1 = min(N, r0 + rps);
+  float ag[8], ab[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ag[e] = 0.f; ab[e] = 0.f; }
+  if (col < d) {
+    for (int r = r0 + phase; r < r1; r += 4) {
+      const size_t off = (size_t)r * d + col;
+      const float mean = RMS ? 0.f : mean_in[r];
+      const float rstd = rstd_in[r];
+      float dyv[8], xv[8];
+      unpack8(ld16<uint4>(dy + off), dyv);
+      unpack8(ld16<uint4>(s + off), xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        ag[e] += dyv[e] * (xv[e] - mean) * rstd;
+        ab[e] += dyv[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][phase][lane * 8 + e] = ag[e];
+    red[1][phase][lane * 8 + e] = ab[e];
+  }
+  __syncthreads();
+  const int P = gridDim.y;
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int gc = blockIdx.x * 512 + c;
+    if (gc < d) {
+      part[(size_t)blockIdx.y * d + gc] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+      if (!RMS)
+        part[(size_t)(P + blockIdx.y) * d + gc] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    }
+  }
+}
+
+// sum P partial rows -> bf16 (overwrite / accumulate); blockIdx.y selects (part0, out0) or
+// (part0 + P*d, out1).  256 threads = 16 column quads x 16 row phases, float4 loads.
 __global__ __launch_bounds__(256) void norm_colreduce_kernel(const float* __restrict__ part, int P,
                                                              int d, bf16_t* __restrict__ gw,
                                                              bf16_t* __restrict__ gb,
                                                              int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= d) return;
-  float a = 0.f, bsum = 0.f;
-  for (int p = 0; p < P; ++p) {
-    a += part[(size_t)p * 2 * d + c];
-    if (gb) bsum += part[(size_t)p * 2 * d + d + c];
+  __shared__ float red[16][65];
+  const float* src = part + (size_t)blockIdx.y * P * d;
+  bf16_t* out = blockIdx.y ? gb : gw;
+  const int cq = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 64 + cq * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c0 < d) {
+    for (int p = ph; p < P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(src + (size_t)p * d + c0);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
   }
-  if (accumulate) {
-    a += bf2f(gw[c]);
-    if (gb) bsum += bf2f(gb[c]);
+  red[ph][cq * 4 + 0] = a.x;
+  red[ph][cq * 4 + 1] = a.y;
+  red[ph][cq * 4 + 2] = a.z;
+  red[ph][cq * 4 + 3] = a.w;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < d) {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+      if (accumulate) t += bf2f(out[c]);
+      out[c] = f2bf(t);
+    }
   }
-  gw[c] = f2bf(a);
-  if (gb) gb[c] = f2bf(bsum);
 }
 
 template <bool RMS, bool HAS_RES>
@@ -264,23 +291,26 @@ void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, v
   }
 }
 
-int dltb_norm_bwd_partials(int N) { return cdiv(N, kWaves * kRowsPerWave); }
+int dltb_norm_bwd_partials(int N) {
+  int P = N / 32;
+  if (P < 1) P = 1;
+  if (P > 128) P = 128;
+  return P;
+}
 
 void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
                    const float* rstd, const void* dres, void* dx, float* part, void* gw, void* gb,
                    int accumulate, int N, int d, bool rms, hipStream_t st) {
   const int nv = nv_for(d);
-  const int P = dltb_norm_bwd_partials(N);
-  dim3 grid(P);
-  size_t lds = (size_t)2 * d * sizeof(float);
   auto DY = (const bf16_t*)dy;
   auto S = (const bf16_t*)s;
   auto W = (const bf16_t*)w;
   auto DR = (const bf16_t*)dres;
   auto DX = (bf16_t*)dx;
+  dim3 grid(cdiv(N, kWaves));
 #define DLTB_NB(NVV, RMSV, RESV)                                                                 \
-  hipLaunchKernelGGL((norm_bwd_kernel<NVV, RMSV, RESV>), grid, dim3(256), lds, st, DY, S, W,     \
-                     mean, rstd, DR, DX, part, N, d)
+  hipLaunchKernelGGL((norm_bwd_dx_kernel<NVV, RMSV, RESV>), grid, dim3(256), 0, st, DY, S, W,    \
+                     mean, rstd, DR, DX, N, d)
 #define DLTB_NB_NV(RMSV, RESV)            \
   switch (nv) {                           \
     case 1: DLTB_NB(1, RMSV, RESV); break; \
@@ -297,6 +327,13 @@ void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* me
   }
 #undef DLTB_NB_NV
 #undef DLTB_NB
-  hipLaunchKernelGGL(norm_colreduce_kernel, dim3(cdiv(d, 256)), dim3(256), 0, st, part, P, d,
+  const int P = dltb_norm_bwd_partials(N);
+  const int rps = cdiv(N, P);
+  dim3 g2(cdiv(d, 512), P);
+  if (rms)
+    hipLaunchKernelGGL(norm_dgamma_kernel<true>, g2, dim3(256), 0, st, DY, S, mean, rstd, part, N, d, rps);
+  else
+    hipLaunchKernelGGL(norm_dgamma_kernel<false>, g2, dim3(256), 0, st, DY, S, mean, rstd, part, N, d, rps);
+  hipLaunchKernelGGL(norm_colreduce_kernel, dim3(cdiv(d, 64), rms ? 1 : 2), dim3(256), 0, st, part, P, d,
                      (bf16_t*)gw, rms ? nullptr : (bf16_t*)gb, accumulate);
 }

@@ -60,7 +60,9 @@ class ReplicatedEngine(Engine):
                 master[ostart:ostart + ln] = master_full[fstart:fstart + ln]
                 opt_segs.append((ostart, ln, self.flat_param[fstart:fstart + ln]))
             self.rs_out = torch.zeros(L.owner_numel, dtype=dt, device=dev) if self.world > 1 else None
-            self.acc = torch.zeros(L.owner_numel, dtype=torch.float32, device=dev) if self.accum > 1 else None
+            # ws == 1: nothing to reduce, gradients accumulate in place in the bf16 flat buffer
+            self.acc = torch.zeros(L.owner_numel, dtype=torch.float32, device=dev) \
+                if (self.accum > 1 and self.world > 1) else None
         else:
             master = master_full
             opt_segs = [(0, L.total, self.flat_param)]
@@ -113,7 +115,7 @@ class ReplicatedEngine(Engine):
 
     # ------------------------------------------------------------------ step lifecycle
     def _on_begin_micro(self):
-        if self.stage == 2:
+        if self.stage == 2 and self.world > 1:
             self._written.clear()         # the full gradient buffer is reduced every micro-step
 
     def _finish_backward(self):

@@ -143,7 +143,7 @@ class ShardedEngine(Engine):
             segs.append((p_chunk, owner - p_chunk, self.shard_buf))
         self.opt = FlatAdamW(master, segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
         self.rs_out = torch.zeros(owner, dtype=dt, device=dev)
-        self.acc = torch.zeros(owner, dtype=torch.float32, device=dev) if self.accum > 1 else None
+        self.acc = torch.zeros(owner, dtype=torch.float32, device=dev) if (self.accum > 1 and self.world > 1) else None
         total_sharded = sum(g.total for g in groups)
         self.keep_all = bool(cfg.max_live_parameters) and total_sharded <= cfg.max_live_parameters and \
             total_sharded <= (cfg.max_reuse_distance or _HUGE)
@@ -289,7 +289,9 @@ class ShardedEngine(Engine):
 
     # ------------------------------------------------------------------ step lifecycle
     def _on_begin_micro(self):
-        self._written.clear()    # full gradient buffers are reduced every micro-step
+        if self.world > 1:
+            self._written.clear()    # full gradient buffers are reduced every micro-step
+        # ws == 1: the group gradient buffers ARE the owner gradients; accumulate in place
 
     def _finish_backward(self):
         if self._p_left != self._p_pending:      # persistent params of units that never reported

@@ -1,0 +1,82 @@
+"""Process-group setup / teardown (reference: setup_distributed / cleanup_distributed,
+train_harness.py:186-204).
+
+Rank / world / local rank come from the torchrun environment (RANK, WORLD_SIZE, LOCAL_RANK,
+MASTER_ADDR, MASTER_PORT) and may be overridden by the reference's explicit CLI flags.  On MI355X
+the backend is "nccl", which on ROCm *is* RCCL (collectives over xGMI); on CPU it is gloo.  Unlike
+the reference, an explicit collective timeout is always passed and the
+single-process case still works for every strategy (the reference's FSDP crashes at WS=1).
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_int(name, default):
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def resolve_ranks(world_size=None, rank=None, local_rank=None):
+    world = world_size if world_size is not None else env_int("WORLD_SIZE", 1)
+    r = rank if rank is not None else env_int("RANK", 0)
+    lr = local_rank if local_rank is not None else env_int("LOCAL_RANK", 0)
+    if os.environ.get("WORLD_SIZE") and world_size is not None and int(os.environ["WORLD_SIZE"]) != world_size:
+        raise ValueError(f"--world-size {world_size} disagrees with WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    return world, r, lr
+
+
+def setup_distributed(world_size, rank, local_rank, master_addr=None, master_port=None,
+                      device_type="cuda", timeout_min=30, debug_collectives=False):
+    """Initialise the process group when world_size > 1; returns the torch.device of this rank."""
+    if device_type == "cuda":
+        if not torch.cuda.is_available():
+            raise RuntimeError("no GPU visible (use --device cpu for the gloo/CPU path)")
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    if world_size > 1 and not dist.is_initialized():
+        if debug_collectives:
+            os.environ["TORCH_DISTRIBUTED_DEBUG"] = "DETAIL"
+        if master_addr:
+            os.environ.setdefault("MASTER_ADDR", master_addr)
+        if master_port:
+            os.environ.setdefault("MASTER_PORT", str(master_port))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        backend = "nccl" if device_type == "cuda" else "gloo"
+        kw = dict(backend=backend, init_method="env://", world_size=world_size, rank=rank,
+                  timeout=datetime.timedelta(minutes=timeout_min))
+        if device_type == "cuda":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+        if device_type == "cuda":      # warm the communicator up outside the timed region
+            t = torch.ones(1, device=device)
+            dist.all_reduce(t)
+            torch.cuda.synchronize(device)
+        print(f"[Rank {rank}/{world_size}] Distributed initialized ({backend})", flush=True)
+    elif world_size == 1:
+        print("Single-GPU mode (no distributed)" if device_type == "cuda" else "Single-process CPU mode",
+              flush=True)
+    return device
+
+
+def cleanup_distributed():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def barrier():
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+def all_reduce_max(x: float, device) -> float:
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+    return x
