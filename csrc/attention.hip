@@ -22,7 +22,12 @@
 // free (D=64: chunk ^ (((r>>1)&1)<<2 | (r>>2)&3); D=128: chunk ^ ((r&3)<<2 | (r>>2)&3)).
 // K/V (or Q/dO) tiles are double-buffered: global loads for tile t+1 are issued into registers
 // before the MFMA work on tile t and written to LDS after it.
-// Dropout uses the counter hash of common.h (row = (b*Hq + h)*T + q, col = key).
+// Dropout uses the counter hash of common.h (row = (b*Hq + h)*T + q, col = key).  The keep-mask is
+// generated ONCE per call by a full-occupancy kernel as packed bits laid out for the forward's lane
+// mapping: word (bh, t, h, q) holds, in bit 16n + i, the decision for key 64t + 32n + (i&3) +
+// 8(i>>2) + 4h of query q — so forward and dQ lanes read one coalesced word per 64-key tile and the
+// dK/dV kernel stages 4 words per query row in LDS.  The hash runs 1x instead of 3x, and the
+// softmax kernels pay 2 VALU ops per probability for dropout.
 #include "common.h"
 
 namespace {
@@ -45,6 +50,7 @@ struct AttnArgs {
   bf16_t* out2;     // bwd_dkdv: dV
   float* lse;
   const float* delta;
+  const uint32_t* mask;   // packed dropout keep-bits (see header), null without dropout
   long q_stride, k_stride, v_stride, o_stride, do_stride, out_stride, out2_stride;
   int B, T, Hq, Hkv;
   float scale;
@@ -142,14 +148,45 @@ DLTB_DEV void store_acc_rows(bf16_t* dst_row, const f32x16* acc, float scale, in
   }
 }
 
+// =============================================================================== dropout mask
+// word (bh, t, h, q) at ((bh*nT + t)*2 + h)*T + q; bit 16n + i <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h
+__global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ mask, long BH, int T,
+                                                        uint32_t thr16, const int64_t* __restrict__ seed_ptr,
+                                                        int64_t site) {
+  const int nT = T / kTile;
+  const long total = BH * nT * 2 * T;
+  const uint64_t seed = site_seed(seed_ptr, site);
+  for (long wi = blockIdx.x * 256L + threadIdx.x; wi < total; wi += (long)gridDim.x * 256) {
+    const int q = (int)(wi % T);
+    long rest = wi / T;
+    const int h = (int)(rest & 1);
+    rest >>= 1;
+    const int t = (int)(rest % nT);
+    const long bh = rest / nT;
+    const uint32_t rk = rng_row_key(seed, (uint32_t)(bh * T + q));
+    uint32_t bits = 0;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        const uint32_t key = (uint32_t)(t * kTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
+        const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
+        bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << (16 * n + i);
+        bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << (16 * n + i + 1);
+      }
+    mask[wi] = bits;
+  }
+}
+
 // =============================================================================== forward
-template <int D>
+template <int D, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
   const int T = P.T;
+  const int nT = T / kTile;
   const int q0 = blockIdx.x * kBlockRows + w * 32;
   const int qi = q0 + r;
 
@@ -159,23 +196,17 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) qf[s] = __builtin_bit_cast(bfx8, ld16<uint4>(qrow + 16 * s + 8 * h));
   }
-  int nt = T / kTile;
-  if (P.causal) nt = min(nt, (blockIdx.x * kBlockRows + kBlockRows - 1) / kTile + 1);
+  int nt = nT;
+  if (CAUSAL) nt = min(nt, (blockIdx.x * kBlockRows + kBlockRows - 1) / kTile + 1);
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
-
-  const bool drop = P.thr16 != 0;
-  uint64_t seed = 0;
-  uint32_t rk = 0;
-  if (drop) {
-    seed = site_seed(P.seed_ptr, P.site);
-    rk = rng_row_key(seed, (uint32_t)(((long)b * P.Hq + hq) * T + qi));
-  }
+  const uint32_t* mrow = DROP ? P.mask + ((long)bh * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
 
   TileLoader<D> lk, lv;
   lk.load(kbase, P.k_stride, 0, tid);
   lv.load(vbase, P.v_stride, 0, tid);
+  uint32_t mw_next = DROP ? mrow[0] : 0u;
   lk.store(smem, tid);
   lv.store(smem + TB, tid);
   __syncthreads();
@@ -183,17 +214,19 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
   f32x16 oacc[D / 32];
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = f32x16{};
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;   // m in scaled log2 units
 
   for (int t = 0; t < nt; ++t) {
     const char* kt = smem + (t & 1) * 2 * TB;
     const char* vt = kt + TB;
+    const uint32_t mw = mw_next;
     if (t + 1 < nt) {
       lk.load(kbase, P.k_stride, (t + 1) * kTile, tid);
       lv.load(vbase, P.v_stride, (t + 1) * kTile, tid);
+      if (DROP) mw_next = mrow[(long)(t + 1) * 2 * T];
     }
     const int kv0 = t * kTile;
-    if (!P.causal || kv0 <= q0 + 31) {
+    if (!CAUSAL || kv0 <= q0 + 31) {
       f32x16 sacc[2];
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
@@ -206,16 +239,16 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          float tv = sacc[n][i] * c;
-          if (P.causal) {
+          float v = sacc[n][i];
+          if (CAUSAL) {
             const int key = kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (key > qi) tv = -INFINITY;
+            if (key > qi) v = -INFINITY;
+            sacc[n][i] = v;
           }
-          sacc[n][i] = tv;
-          mx = fmaxf(mx, tv);
+          mx = fmaxf(mx, v);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
+      const float mnew = fmaxf(m, mx * c);
       const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       m = mnew;
       float ls = 0.f;
@@ -223,24 +256,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(sacc[n][i] - mnew);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[n][i], c, -mnew));
           ls += p;
-          sacc[n][i] = p;
+          sacc[n][i] = (!DROP || ((mw >> (16 * n + i)) & 1u)) ? p : 0.f;
         }
       l = l * alpha + ls;
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) oacc[dt] *= alpha;
-      if (drop) {
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-          for (int i = 0; i < 16; i += 2) {
-            const uint32_t key = (uint32_t)(kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
-            const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
-            sacc[n][i] = keep_lo(hsh, P.thr16) ? sacc[n][i] * P.drop_scale : 0.f;
-            sacc[n][i + 1] = keep_hi(hsh, P.thr16) ? sacc[n][i + 1] * P.drop_scale : 0.f;
-          }
-      }
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
 #pragma unroll
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
     __syncthreads();
   }
   l += __shfl_xor(l, 32, 64);
-  const float inv = 1.f / l;
+  const float inv = (DROP ? P.drop_scale : 1.f) / l;
   bf16_t* orow = P.out + ((long)b * T + qi) * P.out_stride + hq * D;
   store_acc_rows<D>(orow, oacc, inv, h);
   if (h == 0) P.lse[((long)b * P.Hq + hq) * T + qi] = (m + __log2f(l)) * 0.69314718055994531f;
@@ -297,17 +319,27 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs P) {
 
 // =============================================================================== dK / dV
 template <int D>
+constexpr int dkdv_smem_bytes() {
+  return 2 * (2 * kTile * D * 2 + 2 * kTile * 4 + kTile * 16);
+}
+
+template <int D, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
-  constexpr int SB = 2 * TB + 3 * kTile * 4;   // Q tile, dO tile, lse2, delta, rowkey
+  constexpr int SB = dkdv_smem_bytes<D>() / 2;   // Q tile, dO tile, lse2[64], delta[64], mask[64][4]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int bk = blockIdx.y, b = bk / P.Hkv, hk = bk % P.Hkv;
   const int G = P.Hq / P.Hkv;
   const int T = P.T;
+  const int nT = T / kTile;
   const int kblk0 = blockIdx.x * kBlockRows;
   const int k0 = kblk0 + w * 32;
   const int key = k0 + r;
+  // this lane's bit in the packed mask words (see attn_mask_kernel)
+  const int hbit = (r >> 2) & 1;
+  const int jbit = 16 * (w & 1) + ((r & 3) | (((r >> 3) & 3) << 2));
+  const int msub = (w >> 1) * 2 + hbit;
 
   bfx8 kf[D / 16], vf[D / 16];
   {
@@ -323,12 +355,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) { dk[dt] = f32x16{}; dv[dt] = f32x16{}; }
 
-  const bool drop = P.thr16 != 0;
-  const uint64_t seed = drop ? site_seed(P.seed_ptr, P.site) : 0ull;
-  const uint32_t ck = rng_col_key(seed, (uint32_t)key);
   const float c = P.scale * kLog2e;
-  const int t_begin = P.causal ? kblk0 / kTile : 0;
-  const int nt = T / kTile;
+  const int t_begin = CAUSAL ? kblk0 / kTile : 0;
 
   for (int g = 0; g < G; ++g) {
     const int hq = hk * G + g;
@@ -337,44 +365,48 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
     const bf16_t* dobase = P.dout + (long)b * T * P.do_stride + hq * D;
     TileLoader<D> lq, ldo;
     float vl = 0.f, vd = 0.f;
+    uint32_t mword = 0;
     auto load_small = [&](int t) {
       if (tid < kTile) {
         vl = P.lse[bq * T + t * kTile + tid] * kLog2e;
         vd = P.delta[bq * T + t * kTile + tid];
       }
+      if (DROP) {
+        const int row = tid >> 2, sb = tid & 3;
+        mword = P.mask[((bq * nT + (blockIdx.x * 2 + (sb >> 1))) * 2 + (sb & 1)) * T + t * kTile + row];
+      }
     };
-    auto store_small = [&](char* base, int t) {
+    auto store_small = [&](char* base) {
+      float* f = reinterpret_cast<float*>(base + 2 * TB);
       if (tid < kTile) {
-        float* f = reinterpret_cast<float*>(base + 2 * TB);
         f[tid] = vl;
         f[kTile + tid] = vd;
-        reinterpret_cast<uint32_t*>(f)[2 * kTile + tid] =
-            drop ? rng_row_key(seed, (uint32_t)(bq * T + t * kTile + tid)) : 0u;
       }
+      if (DROP) reinterpret_cast<uint32_t*>(f + 2 * kTile)[tid] = mword;
     };
     lq.load(qbase, P.q_stride, t_begin * kTile, tid);
     ldo.load(dobase, P.do_stride, t_begin * kTile, tid);
     load_small(t_begin);
     lq.store(smem, tid);
     ldo.store(smem + TB, tid);
-    store_small(smem, t_begin);
+    store_small(smem);
     __syncthreads();
-    for (int t = t_begin; t < nt; ++t) {
+    for (int t = t_begin; t < nT; ++t) {
       const int bufi = (t - t_begin) & 1;
       const char* qt = smem + bufi * SB;
       const char* dt_ = qt + TB;
       const float* lse2 = reinterpret_cast<const float*>(qt + 2 * TB);
       const float* dlt = lse2 + kTile;
-      const uint32_t* rks = reinterpret_cast<const uint32_t*>(dlt + kTile);
-      if (t + 1 < nt) {
+      const uint32_t* mws = reinterpret_cast<const uint32_t*>(dlt + kTile);
+      if (t + 1 < nT) {
         lq.load(qbase, P.q_stride, (t + 1) * kTile, tid);
         ldo.load(dobase, P.do_stride, (t + 1) * kTile, tid);
         load_small(t + 1);
       }
 #pragma unroll
       for (int mm = 0; mm < 2; ++mm) {
-        const int qbase_abs = t * kTile + 32 * mm;
-        if (P.causal && qbase_abs + 31 < k0) continue;   // every query < every key of this wave
+        const int qb = t * kTile + 32 * mm;
+        if (CAUSAL && qb + 31 < k0) continue;   // every query < every key of this wave
         f32x16 sa = f32x16{}, dp = f32x16{};
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) {
@@ -387,19 +419,21 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
           const int ql = 32 * mm + 8 * g4 + 4 * h;   // rows ql .. ql+3 for regs 4*g4 .. 4*g4+3
           const float4 L = *reinterpret_cast<const float4*>(lse2 + ql);
           const float4 Dl = *reinterpret_cast<const float4*>(dlt + ql);
-          const uint4 RK = *reinterpret_cast<const uint4*>(rks + ql);
           const float Lv[4] = {L.x, L.y, L.z, L.w};
           const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
-          const uint32_t Rv[4] = {RK.x, RK.y, RK.z, RK.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = 4 * g4 + e;
-            float p = __builtin_amdgcn_exp2f(sa[i] * c - Lv[e]);
-            if (P.causal && key > t * kTile + ql + e) p = 0.f;
-            float z = 1.f;
-            if (drop) z = rng_keep(rng_pair(Rv[e], ck), (uint32_t)key, P.thr16) ? P.drop_scale : 0.f;
-            pd[i] = p * z;
-            ds[i] = p * (dp[i] * z - Dv[e]);
+            float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
+            if (CAUSAL && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
+            if (DROP) {
+              const bool keep = (mws[(ql + e) * 4 + msub] >> jbit) & 1u;
+              pd[i] = keep ? p : 0.f;
+              ds[i] = p * ((keep ? dp[i] * P.drop_scale : 0.f) - Dv[e]);
+            } else {
+              pd[i] = p;
+              ds[i] = p * (dp[i] - Dv[e]);
+            }
           }
         }
 #pragma unroll
@@ -413,11 +447,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
           }
         }
       }
-      if (t + 1 < nt) {
+      if (t + 1 < nT) {
         char* nb = smem + ((t + 1 - t_begin) & 1) * SB;
         lq.store(nb, tid);
         ldo.store(nb + TB, tid);
-        store_small(nb, t + 1);
+        store_small(nb);
       }
       __syncthreads();
     }
@@ -425,17 +459,18 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
   bf16_t* dkrow = P.out + ((long)b * T + key) * P.out_stride + hk * D;
   bf16_t* dvrow = P.out2 + ((long)b * T + key) * P.out2_stride + hk * D;
   store_acc_rows<D>(dkrow, dk, P.scale, h);
-  store_acc_rows<D>(dvrow, dv, 1.f, h);
+  store_acc_rows<D>(dvrow, dv, DROP ? P.drop_scale : 1.f, h);
 }
 
 // =============================================================================== dQ
-template <int D>
+template <int D, bool CAUSAL, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
   const int T = P.T;
+  const int nT = T / kTile;
   const int q0 = blockIdx.x * kBlockRows + w * 32;
   const int qi = q0 + r;
   const long bq = (long)b * P.Hq + hq;
@@ -452,22 +487,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs P) {
   }
   const float lse2 = P.lse[bq * T + qi] * kLog2e;
   const float dl = P.delta[bq * T + qi];
-  const bool drop = P.thr16 != 0;
-  uint64_t seed = 0;
-  uint32_t rk = 0;
-  if (drop) {
-    seed = site_seed(P.seed_ptr, P.site);
-    rk = rng_row_key(seed, (uint32_t)(bq * T + qi));
-  }
+  const uint32_t* mrow = DROP ? P.mask + ((long)bq * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
-  int nt = T / kTile;
-  if (P.causal) nt = min(nt, (blockIdx.x * kBlockRows + kBlockRows - 1) / kTile + 1);
+  int nt = nT;
+  if (CAUSAL) nt = min(nt, (blockIdx.x * kBlockRows + kBlockRows - 1) / kTile + 1);
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
 
   TileLoader<D> lk, lv;
   lk.load(kbase, P.k_stride, 0, tid);
   lv.load(vbase, P.v_stride, 0, tid);
+  uint32_t mw_next = DROP ? mrow[0] : 0u;
   lk.store(smem, tid);
   lv.store(smem + TB, tid);
   __syncthreads();
@@ -479,14 +509,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs P) {
   for (int t = 0; t < nt; ++t) {
     const char* kt = smem + (t & 1) * 2 * TB;
     const char* vt = kt + TB;
+    const uint32_t mw = mw_next;
     if (t + 1 < nt) {
       lk.load(kbase, P.k_stride, (t + 1) * kTile, tid);
       lv.load(vbase, P.v_stride, (t + 1) * kTile, tid);
+      if (DROP) mw_next = mrow[(long)(t + 1) * 2 * T];
     }
     const int kv0 = t * kTile;
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-      if (P.causal && kv0 + 32 * n > q0 + 31) continue;
+      if (CAUSAL && kv0 + 32 * n > q0 + 31) continue;
       f32x16 sa = f32x16{}, dp = f32x16{};
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
@@ -495,22 +527,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs P) {
       }
       f32x16 ds;
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const int keyi = kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float p0 = __builtin_amdgcn_exp2f(sa[i] * c - lse2);
-        float p1 = __builtin_amdgcn_exp2f(sa[i + 1] * c - lse2);
-        if (P.causal) {
-          if (keyi > qi) p0 = 0.f;
-          if (keyi + 1 > qi) p1 = 0.f;
-        }
-        float z0 = 1.f, z1 = 1.f;
-        if (drop) {
-          const uint32_t hsh = rng_pair(rk, rng_col_key(seed, (uint32_t)keyi));
-          z0 = keep_lo(hsh, P.thr16) ? P.drop_scale : 0.f;
-          z1 = keep_hi(hsh, P.thr16) ? P.drop_scale : 0.f;
-        }
-        ds[i] = p0 * (dp[i] * z0 - dl);
-        ds[i + 1] = p1 * (dp[i + 1] * z1 - dl);
+      for (int i = 0; i < 16; ++i) {
+        float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -lse2));
+        if (CAUSAL && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
+        float dpv = dp[i];
+        if (DROP) dpv = ((mw >> (16 * n + i)) & 1u) ? dpv * P.drop_scale : 0.f;
+        ds[i] = p * (dpv - dl);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -558,77 +580,132 @@ AttnArgs make_args(const void* q, const void* k, const void* v, long qs, long ks
 
 bool dltb_attn_supported(int D, int T) { return (D == 64 || D == 128) && T % kBlockRows == 0; }
 
-void dltb_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, long qs,
-                   long ks, long vs, long os, int B, int T, int Hq, int Hkv, int D, float scale,
-                   int causal, uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
+long dltb_attn_mask_words(int B, int Hq, int T) { return (long)B * Hq * (T / kTile) * 2 * T; }
+
+namespace {
+
+template <int D, bool C, bool DR>
+void set_attrs() {
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, C, DR>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTile * D * 2);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTile * D * 2);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, C, DR>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, dkdv_smem_bytes<D>());
+}
+
+template <int D, bool C, bool DR>
+void launch_fwd(const AttnArgs& a, hipStream_t st) {
+  dim3 grid(a.T / kBlockRows, a.B * a.Hq);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, C, DR>), grid, dim3(256), 4 * kTile * D * 2, st, a);
+}
+
+template <int D, bool C, bool DR>
+void launch_bwd(const AttnArgs& a, const AttnArgs& kv, hipStream_t st) {
+  dim3 gkv(a.T / kBlockRows, a.B * a.Hkv);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR>), gkv, dim3(256), dkdv_smem_bytes<D>(), st, kv);
+  dim3 gq(a.T / kBlockRows, a.B * a.Hq);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR>), gq, dim3(256), 4 * kTile * D * 2, st, a);
+}
+
+#define DLTB_ATTN_DISPATCH(FN, D, C, DR, ...)           \
+  do {                                                  \
+    if (D == 64) {                                      \
+      if (C) { if (DR) FN<64, true, true>(__VA_ARGS__); else FN<64, true, false>(__VA_ARGS__); } \
+      else   { if (DR) FN<64, false, true>(__VA_ARGS__); else FN<64, false, false>(__VA_ARGS__); } \
+    } else {                                            \
+      if (C) { if (DR) FN<128, true, true>(__VA_ARGS__); else FN<128, true, false>(__VA_ARGS__); } \
+      else   { if (DR) FN<128, false, true>(__VA_ARGS__); else FN<128, false, false>(__VA_ARGS__); } \
+    }                                                   \
+  } while (0)
+
+}  // namespace
+
+void dltb_attn_init_attributes() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  set_attrs<64, false, false>();
+  set_attrs<64, false, true>();
+  set_attrs<64, true, false>();
+  set_attrs<64, true, true>();
+  set_attrs<128, false, false>();
+  set_attrs<128, false, true>();
+  set_attrs<128, true, false>();
+  set_attrs<128, true, true>();
+}
+
+void dltb_attn_mask(uint32_t* mask, int B, int T, int Hq, uint32_t thr16, const int64_t* seed,
+                    int64_t site, hipStream_t st) {
+  const long words = dltb_attn_mask_words(B, Hq, T);
+  long g = (words + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(attn_mask_kernel, dim3(g), dim3(256), 0, st, mask, (long)B * Hq, T, thr16, seed, site);
+}
+
+void dltb_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                   const uint32_t* mask, long qs, long ks, long vs, long os, int B, int T, int Hq,
+                   int Hkv, int D, float scale, int causal, uint32_t thr16, float drop_scale,
                    hipStream_t st) {
   AttnArgs a = make_args(q, k, v, qs, ks, vs, B, T, Hq, Hkv, scale, causal, thr16, drop_scale,
-                         seed, site);
+                         nullptr, 0);
   a.out = (bf16_t*)o;
   a.out_stride = os;
   a.lse = lse;
-  dim3 grid(T / kBlockRows, B * Hq);
-  if (D == 64)
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 4 * kTile * 64 * 2, st, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, dim3(256), 4 * kTile * 128 * 2, st, a);
+  a.mask = mask;
+  DLTB_ATTN_DISPATCH(launch_fwd, D, causal != 0, thr16 != 0, a, st);
 }
 
-void dltb_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                   const float* lse, float* delta, void* dq, void* dk, void* dv, long qs, long ks,
-                   long vs, long os, long dos, long dqs, long dks, long dvs, int B, int T, int Hq,
-                   int Hkv, int D, float scale, int causal, uint32_t thr16, float drop_scale,
-                   const int64_t* seed, int64_t site, hipStream_t st) {
-  AttnArgs a = make_args(q, k, v, qs, ks, vs, B, T, Hq, Hkv, scale, causal, thr16, drop_scale,
-                         seed, site);
+void dltb_attn_bwd_delta(const void* o, const void* dout, float* delta, long os, long dos, int B,
+                         int T, int Hq, int D, hipStream_t st) {
+  AttnArgs a{};
   a.o = (const bf16_t*)o;
   a.o_stride = os;
   a.dout = (const bf16_t*)dout;
   a.do_stride = dos;
-  a.lse = const_cast<float*>(lse);
   a.delta = delta;
+  a.B = B;
+  a.T = T;
+  a.Hq = Hq;
   const long rows = (long)B * T * Hq * (D / 8);
   if (D == 64)
     hipLaunchKernelGGL(attn_bwd_delta_kernel<64>, dim3(cdiv(rows, 256)), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(attn_bwd_delta_kernel<128>, dim3(cdiv(rows, 256)), dim3(256), 0, st, a);
-  // dK, dV (key-major)
-  AttnArgs b = a;
-  b.out = (bf16_t*)dk;
-  b.out_stride = dks;
-  b.out2 = (bf16_t*)dv;
-  b.out2_stride = dvs;
-  dim3 gkv(T / kBlockRows, B * Hkv);
-  const int sb64 = 2 * (2 * kTile * 64 * 2 + 3 * kTile * 4);
-  const int sb128 = 2 * (2 * kTile * 128 * 2 + 3 * kTile * 4);
-  if (D == 64)
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<64>, gkv, dim3(256), sb64, st, b);
-  else
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<128>, gkv, dim3(256), sb128, st, b);
-  // dQ (query-major)
-  AttnArgs c = a;
-  c.out = (bf16_t*)dq;
-  c.out_stride = dqs;
-  dim3 gq(T / kBlockRows, B * Hq);
-  if (D == 64)
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, gq, dim3(256), 4 * kTile * 64 * 2, st, c);
-  else
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<128>, gq, dim3(256), 4 * kTile * 128 * 2, st, c);
 }
 
-// Kernels asking for more than 64 KiB of dynamic LDS must opt in (MI355X has 160 KiB per CU).
-void dltb_attn_init_attributes() {
-  static bool done = false;
-  if (done) return;
-  done = true;
-  const int sb128 = 2 * (2 * kTile * 128 * 2 + 3 * kTile * 4);
-  const int sb64 = 2 * (2 * kTile * 64 * 2 + 3 * kTile * 4);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<128>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, sb128);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<64>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, sb64);
-  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<128>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTile * 128 * 2);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<128>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTile * 128 * 2);
+namespace {
+template <int D, bool C, bool DR>
+void launch_dkdv(const AttnArgs& a, hipStream_t st) {
+  dim3 gkv(a.T / kBlockRows, a.B * a.Hkv);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR>), gkv, dim3(256), dkdv_smem_bytes<D>(), st, a);
+}
+template <int D, bool C, bool DR>
+void launch_dq(const AttnArgs& a, hipStream_t st) {
+  dim3 gq(a.T / kBlockRows, a.B * a.Hq);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR>), gq, dim3(256), 4 * kTile * D * 2, st, a);
+}
+}  // namespace
+
+// part: 0 = dK/dV (key-major kernel), 1 = dQ (query-major kernel); both need delta
+void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, const void* dout,
+                        const float* lse, const float* delta, const uint32_t* mask, void* out,
+                        void* out2, long qs, long ks, long vs, long dos, long outs, long out2s,
+                        int B, int T, int Hq, int Hkv, int D, float scale, int causal,
+                        uint32_t thr16, float drop_scale, hipStream_t st) {
+  AttnArgs a = make_args(q, k, v, qs, ks, vs, B, T, Hq, Hkv, scale, causal, thr16, drop_scale,
+                         nullptr, 0);
+  a.dout = (const bf16_t*)dout;
+  a.do_stride = dos;
+  a.lse = const_cast<float*>(lse);
+  a.delta = delta;
+  a.mask = mask;
+  a.out = (bf16_t*)out;
+  a.out_stride = outs;
+  a.out2 = (bf16_t*)out2;
+  a.out2_stride = out2s;
+  if (part == 0)
+    DLTB_ATTN_DISPATCH(launch_dkdv, D, causal != 0, thr16 != 0, a, st);
+  else
+    DLTB_ATTN_DISPATCH(launch_dq, D, causal != 0, thr16 != 0, a, st);
 }

@@ -337,48 +337,142 @@ void check_attn_view(const Tensor& t, const char* name, int64_t rows, int64_t he
   check_align16(t, name);
 }
 
-std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, int64_t B,
-                             int64_t T, int64_t Hq, int64_t Hkv, double scale, bool causal,
-                             double p, const optional<Tensor>& seed, int64_t site) {
+void check_lse(const Tensor& t, int64_t n, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.numel() == n && t.is_contiguous(), name, " f32 [B,Hq,T]");
+}
+
+const uint32_t* mask_ptr(const optional<Tensor>& mask, uint32_t thr, int64_t B, int64_t T, int64_t Hq) {
+  if (!thr) return nullptr;
+  TORCH_CHECK(mask.has_value() && mask->is_cuda() && mask->scalar_type() == at::kInt &&
+                  mask->numel() == dltb_attn_mask_words((int)B, (int)Hq, (int)T),
+              "attention with dropout needs the packed mask of attn_mask()");
+  return reinterpret_cast<const uint32_t*>(mask->data_ptr<int>());
+}
+
+int64_t attn_head_dim(const Tensor& q, int64_t B, int64_t T, int64_t Hq) {
   const int64_t D = q.size(1) / Hq;
   TORCH_CHECK(dltb_attn_supported((int)D, (int)T), "attention: needs D in {64,128} and T % 128 == 0");
+  return D;
+}
+
+Tensor attn_mask(int64_t B, int64_t T, int64_t Hq, double p, const Tensor& seed, int64_t site,
+                 const Tensor& like) {
+  TORCH_CHECK(T % 128 == 0 && p > 0.0, "attn_mask: T % 128 and p > 0");
+  auto mask = at::empty({dltb_attn_mask_words((int)B, (int)Hq, (int)T)}, like.options().dtype(at::kInt));
+  dltb_attn_mask(reinterpret_cast<uint32_t*>(mask.data_ptr<int>()), (int)B, (int)T, (int)Hq, thr_of(p),
+                 seed_ptr(seed, p), site, cur_stream());
+  return mask;
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v,
+                             const optional<Tensor>& mask, int64_t B, int64_t T, int64_t Hq,
+                             int64_t Hkv, double scale, bool causal, double p) {
+  const int64_t D = attn_head_dim(q, B, T, Hq);
   TORCH_CHECK(Hq % Hkv == 0, "attention: Hq % Hkv");
   check_attn_view(q, "q", B * T, Hq, D);
   check_attn_view(k, "k", B * T, Hkv, D);
   check_attn_view(v, "v", B * T, Hkv, D);
+  const uint32_t thr = thr_of(p);
+  const uint32_t* mp = mask_ptr(mask, thr, B, T, Hq);
   dltb_attn_init_attributes();
   auto o = at::empty({B * T, Hq * D}, q.options());
   auto lse = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
-  dltb_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
-                q.stride(0), k.stride(0), v.stride(0), o.stride(0), (int)B, (int)T, (int)Hq,
-                (int)Hkv, (int)D, (float)scale, causal ? 1 : 0, thr_of(p), scale_of(p),
-                seed_ptr(seed, p), site, cur_stream());
+  dltb_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), mp,
+                q.stride(0), k.stride(0), v.stride(0), o.stride(0), (int)B, (int)T, (int)Hq, (int)Hkv,
+                (int)D, (float)scale, causal ? 1 : 0, thr, scale_of(p), cur_stream());
   return {o, lse};
 }
 
-void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,
-              const Tensor& lse, const Tensor& dq, const Tensor& dk, const Tensor& dv, int64_t B,
-              int64_t T, int64_t Hq, int64_t Hkv, double scale, bool causal, double p,
-              const optional<Tensor>& seed, int64_t site) {
-  const int64_t D = q.size(1) / Hq;
-  TORCH_CHECK(dltb_attn_supported((int)D, (int)T), "attention: needs D in {64,128} and T % 128 == 0");
+Tensor attn_bwd_delta(const Tensor& o, const Tensor& dout, int64_t B, int64_t T, int64_t Hq) {
+  const int64_t D = attn_head_dim(o, B, T, Hq);
+  check_attn_view(o, "o", B * T, Hq, D);
+  check_attn_view(dout, "dout", B * T, Hq, D);
+  auto delta = at::empty({B, Hq, T}, o.options().dtype(at::kFloat));
+  dltb_attn_bwd_delta(o.data_ptr(), dout.data_ptr(), delta.data_ptr<float>(), o.stride(0),
+                      dout.stride(0), (int)B, (int)T, (int)Hq, (int)D, cur_stream());
+  return delta;
+}
+
+// part 0: dK, dV (out = dk, out2 = dv); part 1: dQ (out = dq)
+void attn_bwd_part(int64_t part, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& dout,
+                   const Tensor& lse, const Tensor& delta, const optional<Tensor>& mask,
+                   const Tensor& out, const optional<Tensor>& out2, int64_t B, int64_t T, int64_t Hq,
+                   int64_t Hkv, double scale, bool causal, double p) {
+  const int64_t D = attn_head_dim(q, B, T, Hq);
   check_attn_view(q, "q", B * T, Hq, D);
   check_attn_view(k, "k", B * T, Hkv, D);
   check_attn_view(v, "v", B * T, Hkv, D);
-  check_attn_view(o, "o", B * T, Hq, D);
   check_attn_view(dout, "dout", B * T, Hq, D);
-  check_attn_view(dq, "dq", B * T, Hq, D);
-  check_attn_view(dk, "dk", B * T, Hkv, D);
-  check_attn_view(dv, "dv", B * T, Hkv, D);
-  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.numel() == B * Hq * T && lse.is_contiguous(), "lse");
+  check_lse(lse, B * Hq * T, "lse");
+  check_lse(delta, B * Hq * T, "delta");
+  if (part == 0) {
+    TORCH_CHECK(out2.has_value(), "dkdv needs dv");
+    check_attn_view(out, "dk", B * T, Hkv, D);
+    check_attn_view(*out2, "dv", B * T, Hkv, D);
+  } else {
+    check_attn_view(out, "dq", B * T, Hq, D);
+  }
+  const uint32_t thr = thr_of(p);
+  const uint32_t* mp = mask_ptr(mask, thr, B, T, Hq);
   dltb_attn_init_attributes();
-  auto delta = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
-  dltb_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(),
-                lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
-                dv.data_ptr(), q.stride(0), k.stride(0), v.stride(0), o.stride(0), dout.stride(0),
-                dq.stride(0), dk.stride(0), dv.stride(0), (int)B, (int)T, (int)Hq, (int)Hkv, (int)D,
-                (float)scale, causal ? 1 : 0, thr_of(p), scale_of(p), seed_ptr(seed, p), site,
-                cur_stream());
+  dltb_attn_bwd_part((int)part, q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(),
+                     lse.data_ptr<float>(), delta.data_ptr<float>(), mp, out.data_ptr(),
+                     part == 0 ? out2->data_ptr() : nullptr, q.stride(0), k.stride(0), v.stride(0),
+                     dout.stride(0), out.stride(0), part == 0 ? out2->stride(0) : 0, (int)B, (int)T,
+                     (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0, thr, scale_of(p),
+                     cur_stream());
+}
+
+void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,
+              const Tensor& lse, const optional<Tensor>& mask, const Tensor& dq, const Tensor& dk,
+              const Tensor& dv, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, double scale, bool causal,
+              double p) {
+  auto delta = attn_bwd_delta(o, dout, B, T, Hq);
+  attn_bwd_part(0, q, k, v, dout, lse, delta, mask, dk, dv, B, T, Hq, Hkv, scale, causal, p);
+  attn_bwd_part(1, q, k, v, dout, lse, delta, mask, dq, c10::nullopt, B, T, Hq, Hkv, scale, causal, p);
+}
+
+Tensor norm_bwd_dx(const Tensor& dy, const Tensor& s, const Tensor& w, const optional<Tensor>& mean,
+                   const Tensor& rstd, const optional<Tensor>& dres, bool rms) {
+  check_contig_bf16(dy, "dy");
+  check_contig_bf16(s, "s");
+  check_contig_bf16(w, "w");
+  const int64_t d = dy.size(-1);
+  const int64_t N = dy.numel() / d;
+  TORCH_CHECK(d % 8 == 0 && d <= 4096 && s.sizes() == dy.sizes() && w.numel() == d, "norm_bwd_dx shapes");
+  TORCH_CHECK(rstd.numel() == N && (rms || (mean.has_value() && mean->numel() == N)), "norm stats");
+  if (dres.has_value()) {
+    check_contig_bf16(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == dy.sizes(), "norm_bwd_dx: dres shape");
+  }
+  auto dx = at::empty_like(dy);
+  dltb_norm_bwd_dx(dy.data_ptr(), s.data_ptr(), w.data_ptr(), rms ? nullptr : mean->data_ptr<float>(),
+                   rstd.data_ptr<float>(), dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(),
+                   (int)N, (int)d, rms, cur_stream());
+  return dx;
+}
+
+void norm_bwd_dgamma(const Tensor& dy, const Tensor& s, const optional<Tensor>& mean, const Tensor& rstd,
+                     const Tensor& gw, const optional<Tensor>& gb, bool accumulate, bool rms) {
+  check_contig_bf16(dy, "dy");
+  check_contig_bf16(s, "s");
+  check_contig_bf16(gw, "gw");
+  const int64_t d = dy.size(-1);
+  const int64_t N = dy.numel() / d;
+  TORCH_CHECK(s.sizes() == dy.sizes() && gw.numel() == d, "norm_bwd_dgamma shapes");
+  TORCH_CHECK(rstd.numel() == N && (rms || (mean.has_value() && mean->numel() == N)), "norm stats");
+  if (!rms) {
+    TORCH_CHECK(gb.has_value(), "layernorm needs gb");
+    check_contig_bf16(*gb, "gb");
+    TORCH_CHECK(gb->numel() == d, "gb size");
+  }
+  const int P = dltb_norm_bwd_partials((int)N);
+  auto part = at::empty({(int64_t)P * 2 * d}, dy.options().dtype(at::kFloat));
+  dltb_norm_bwd_dgamma(dy.data_ptr(), s.data_ptr(), rms ? nullptr : mean->data_ptr<float>(),
+                       rstd.data_ptr<float>(), part.data_ptr<float>(), gw.data_ptr(),
+                       rms ? nullptr : gb->data_ptr(), accumulate ? 1 : 0, (int)N, (int)d, rms,
+                       cur_stream());
 }
 
 }  // namespace
@@ -402,7 +496,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_chunk", &dltb_adamw_chunk);
   m.def("sumsq_", &sumsq_);
   m.def("clip_coef", &clip_coef);
+  m.def("attn_mask", &attn_mask);
   m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd_delta", &attn_bwd_delta);
+  m.def("attn_bwd_part", &attn_bwd_part);
   m.def("attn_bwd", &attn_bwd);
+  m.def("norm_bwd_dx", &norm_bwd_dx);
+  m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
   m.def("arch", []() { return std::string("gfx950"); });
 }

@@ -10,6 +10,12 @@ void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, v
                    uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
                    hipStream_t st);
 int dltb_norm_bwd_partials(int N);
+void dltb_norm_bwd_dx(const void* dy, const void* s, const void* w, const float* mean,
+                      const float* rstd, const void* dres, void* dx, int N, int d, bool rms,
+                      hipStream_t st);
+void dltb_norm_bwd_dgamma(const void* dy, const void* s, const float* mean, const float* rstd,
+                          float* part, void* gw, void* gb, int accumulate, int N, int d, bool rms,
+                          hipStream_t st);
 void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
                    const float* rstd, const void* dres, void* dx, float* part, void* gw, void* gb,
                    int accumulate, int N, int d, bool rms, hipStream_t st);
@@ -58,13 +64,18 @@ void dltb_fill_f32(float* x, long n, float v, hipStream_t st);
 
 // attention.hip
 bool dltb_attn_supported(int D, int T);
-void dltb_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, long qs,
-                   long ks, long vs, long os, int B, int T, int Hq, int Hkv, int D, float scale,
-                   int causal, uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
-                   hipStream_t st);
-void dltb_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                   const float* lse, float* delta, void* dq, void* dk, void* dv, long qs, long ks,
-                   long vs, long os, long dos, long dqs, long dks, long dvs, int B, int T, int Hq,
+long dltb_attn_mask_words(int B, int Hq, int T);
+void dltb_attn_mask(uint32_t* mask, int B, int T, int Hq, uint32_t thr16, const int64_t* seed,
+                    int64_t site, hipStream_t st);
+void dltb_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
+                   const uint32_t* mask, long qs, long ks, long vs, long os, int B, int T, int Hq,
                    int Hkv, int D, float scale, int causal, uint32_t thr16, float drop_scale,
-                   const int64_t* seed, int64_t site, hipStream_t st);
+                   hipStream_t st);
+void dltb_attn_bwd_delta(const void* o, const void* dout, float* delta, long os, long dos, int B,
+                         int T, int Hq, int D, hipStream_t st);
+void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, const void* dout,
+                        const float* lse, const float* delta, const uint32_t* mask, void* out,
+                        void* out2, long qs, long ks, long vs, long dos, long outs, long out2s,
+                        int B, int T, int Hq, int Hkv, int D, float scale, int causal,
+                        uint32_t thr16, float drop_scale, hipStream_t st);
 void dltb_attn_init_attributes();

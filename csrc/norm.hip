@@ -298,9 +298,9 @@ int dltb_norm_bwd_partials(int N) {
   return P;
 }
 
-void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
-                   const float* rstd, const void* dres, void* dx, float* part, void* gw, void* gb,
-                   int accumulate, int N, int d, bool rms, hipStream_t st) {
+void dltb_norm_bwd_dx(const void* dy, const void* s, const void* w, const float* mean,
+                      const float* rstd, const void* dres, void* dx, int N, int d, bool rms,
+                      hipStream_t st) {
   const int nv = nv_for(d);
   auto DY = (const bf16_t*)dy;
   auto S = (const bf16_t*)s;
@@ -327,6 +327,13 @@ void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* me
   }
 #undef DLTB_NB_NV
 #undef DLTB_NB
+}
+
+void dltb_norm_bwd_dgamma(const void* dy, const void* s, const float* mean, const float* rstd,
+                          float* part, void* gw, void* gb, int accumulate, int N, int d, bool rms,
+                          hipStream_t st) {
+  auto DY = (const bf16_t*)dy;
+  auto S = (const bf16_t*)s;
   const int P = dltb_norm_bwd_partials(N);
   const int rps = cdiv(N, P);
   dim3 g2(cdiv(d, 512), P);
@@ -336,4 +343,11 @@ void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* me
     hipLaunchKernelGGL(norm_dgamma_kernel<false>, g2, dim3(256), 0, st, DY, S, mean, rstd, part, N, d, rps);
   hipLaunchKernelGGL(norm_colreduce_kernel, dim3(cdiv(d, 64), rms ? 1 : 2), dim3(256), 0, st, part, P, d,
                      (bf16_t*)gw, rms ? nullptr : (bf16_t*)gb, accumulate);
+}
+
+void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
+                   const float* rstd, const void* dres, void* dx, float* part, void* gw, void* gb,
+                   int accumulate, int N, int d, bool rms, hipStream_t st) {
+  dltb_norm_bwd_dx(dy, s, w, mean, rstd, dres, dx, N, d, rms, st);
+  dltb_norm_bwd_dgamma(dy, s, mean, rstd, part, gw, gb, accumulate, N, d, rms, st);
 }

@@ -27,6 +27,7 @@ import torch
 import torch.nn as nn
 
 from ..ops import functional as F_
+from ..ops.streams import GradStreams
 from ..parallel.runtime import EAGER, Unit
 from .config import ModelConfig
 
@@ -98,10 +99,13 @@ class _BlockFn(torch.autograd.Function):
         cfg = model.cfg
         H, d = cfg.n_head, cfg.n_embd
         p = model.drop_p
+        par = GradStreams(x.device)
+        amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x, par)   # overlaps LN1 + QKV GEMM
         _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False)
         qkv = F_.linear_fwd(h1, win, bin_)
-        o, lse = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
-                             1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
+        o, lse, amask = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
+                                    1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i),
+                                    amask, par)
         a = F_.linear_fwd(o, wo, bo)
         x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False)
         f = F_.linear_fwd(h2, w1, b1)
@@ -110,14 +114,14 @@ class _BlockFn(torch.autograd.Function):
         x2 = F_.dropout(x1, m, p, rt.seed, model.site_mlp(i))
         rt.release_forward(unit)
         ctx.model, ctx.i = model, i
-        ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, x1, h2, mean2, rstd2, f, g)
+        ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g)
         return x2
 
     @staticmethod
     def backward(ctx, dx2):
         model, i = ctx.model, ctx.i
         rt, unit = model.rt, model.unit_blocks[i]
-        (x, h1, mean1, rstd1, qkv, o, lse, x1, h2, mean2, rstd2, f, g) = ctx.saved
+        (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g) = ctx.saved
         ctx.saved = None
         (ln1w, ln1b, win, bin_, wo, bo, ln2w, ln2b, w1, b1, w2, b2) = rt.acquire_backward(unit)
         B, T = model._cur_bt
@@ -126,24 +130,27 @@ class _BlockFn(torch.autograd.Function):
         p = model.drop_p
         dx2 = dx2.contiguous()
         s = [rt.grad_slot(unit, j) for j in range(12)]
+        par = GradStreams(dx2.device)      # parameter-gradient work -> side stream
         # MLP
         dm = F_.dropout(None, dx2, p, rt.seed, model.site_mlp(i))
-        F_.linear_wgrad(dm, g, s[10][0], s[11][0], s[10][1])
+        F_.linear_wgrad(dm, g, s[10][0], s[11][0], s[10][1], par)
         dg = torch.mm(dm, w2)
         df = F_.gelu_bwd(dg, f, s[9][0], s[9][1])
-        F_.linear_wgrad(df, h2, s[8][0], None, s[8][1])
+        F_.linear_wgrad(df, h2, s[8][0], None, s[8][1], par)
         dh2 = torch.mm(df, w1)
-        dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False)
+        dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False, par)
         # attention
-        F_.linear_wgrad(dx1, o, s[4][0], s[5][0], s[4][1])
+        F_.linear_wgrad(dx1, o, s[4][0], s[5][0], s[4][1], par)
         do = torch.mm(dx1, wo)
         dqkv = torch.empty_like(qkv)
-        F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse,
+        F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, amask,
                     dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
-                    1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
-        F_.linear_wgrad(dqkv, h1, s[2][0], s[3][0], s[2][1])
+                    1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i), par)
+        par.join()                                            # dQ (side) completes dqkv
+        F_.linear_wgrad(dqkv, h1, s[2][0], s[3][0], s[2][1], par)
         dh1 = torch.mm(dqkv, win)
-        dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False)
+        dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False, par)
+        par.join()                                            # all of this unit's gradients written
         rt.grads_ready(unit)
         rt.release_backward(unit)
         return dx, None, None
@@ -185,13 +192,15 @@ class _HeadFn(torch.autograd.Function):
         lnw, lnb = rt.acquire_backward(model.unit_head)
         wte = rt.acquire_tied(model.unit_embed)[0]
         g = (dloss.to(torch.float32) / count)
+        par = GradStreams(x.device)
         dw, acc_w = rt.grad_slot(model.unit_embed, 0)            # tied lm_head / wte
         hs = (h * g).to(h.dtype)
-        F_.linear_wgrad(dl, hs, dw, None, acc_w)
+        F_.linear_wgrad(dl, hs, dw, None, acc_w, par)              # side stream, overlaps dh
         dh = (torch.mm(dl, wte) * g).to(h.dtype)
         gw, acc = rt.grad_slot(model.unit_head, 0)
         gb, _ = rt.grad_slot(model.unit_head, 1)
-        dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False)
+        dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False, par)
+        par.join()
         rt.grads_ready(model.unit_head)
         rt.release_backward(model.unit_head)
         return dx, None, None, None

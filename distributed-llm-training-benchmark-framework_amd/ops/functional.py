@@ -27,9 +27,16 @@ def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0):
     return ref.norm_fwd(x, r, w, b, eps, rms, p, seed, site)
 
 
-def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms):
+def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None):
+    """dx on the current stream; dgamma/dbeta (parameter gradients) on ``par``'s side stream."""
     if _gpu(dy):
-        return ext().norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
+        C = ext()
+        if par is None or not par.enabled:
+            return C.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
+        dx = C.norm_bwd_dx(dy, s, w, mean, rstd, dres, rms)
+        with par.fork(dy, s, mean, rstd):
+            C.norm_bwd_dgamma(dy, s, mean, rstd, gw, gb, accumulate, rms)
+        return dx
     return ref.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
 
 
@@ -94,18 +101,45 @@ def xent_fwd_bwd_(logits2d, targets1d, ignore_index=-1):
 
 
 # ------------------------------------------------------------------------------ attention
-def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site):
-    if _gpu(q):
-        o, lse = ext().attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p,
-                                _sd(seed) if p > 0 else None, site)
-        return o, lse
-    return ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site)
+def attn_mask(B, T, Hq, p, seed, site, like, par=None):
+    """Packed dropout keep-bits for attention (GPU only; launched on the side stream so it overlaps
+    the QKV projection).  Returns None on the CPU or without dropout."""
+    if p <= 0 or not like.is_cuda:
+        return None
+    if par is not None and par.enabled:
+        with par.fork():
+            m = ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, like)
+        m.record_stream(par.main)
+        return m
+    return ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, like)
 
 
-def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site):
+def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site, mask=None, par=None):
+    """Returns (o, lse, aux); ``aux`` (the packed dropout mask on the GPU) goes back into attn_bwd."""
     if _gpu(q):
-        ext().attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p,
-                       _sd(seed) if p > 0 else None, site)
+        if p > 0 and mask is None:
+            mask = ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, q)
+        if par is not None:
+            par.join()                      # the mask was produced on the side stream
+        o, lse = ext().attn_fwd(q, k, v, mask if p > 0 else None, B, T, Hq, Hkv, scale, causal, p)
+        return o, lse, (mask if p > 0 else None)
+    o, lse = ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site)
+    return o, lse, None
+
+
+def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site, par=None):
+    """dK/dV (key-major kernel) on the current stream, dQ (query-major kernel) concurrently on
+    ``par``'s side stream.  Call ``par.join()`` before reading dq."""
+    if _gpu(q):
+        C = ext()
+        delta = C.attn_bwd_delta(o, do, B, T, Hq)
+        m = aux if p > 0 else None
+        if par is not None and par.enabled:
+            with par.fork(q, k, v, do, lse, delta, m):
+                C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p)
+        else:
+            C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p)
+        C.attn_bwd_part(0, q, k, v, do, lse, delta, m, dk, dv, B, T, Hq, Hkv, scale, causal, p)
     else:
         ref.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site)
 
@@ -117,8 +151,13 @@ def linear_fwd(x2d, w, b=None):
     return torch.addmm(b, x2d, w.t())
 
 
-def linear_wgrad(dy2d, x2d, dw, db, accumulate):
-    """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy)."""
+def linear_wgrad(dy2d, x2d, dw, db, accumulate, par=None):
+    """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy).  With ``par`` the
+    work runs on the side stream (parameter gradients are off the critical path)."""
+    if par is not None and par.enabled:
+        with par.fork(dy2d, x2d):
+            linear_wgrad(dy2d, x2d, dw, db, accumulate)
+        return
     if dw is not None:
         if accumulate:
             dw.addmm_(dy2d.t(), x2d)

@@ -181,7 +181,8 @@ def test_attention(B, T, Hq, Hkv, D, causal, p):
     q, k, v = qkv[:, :Hq * D], qkv[:, Hq * D:(Hq + Hkv) * D], qkv[:, (Hq + Hkv) * D:]
     scale = 1.0 / math.sqrt(D)
     sd = seed_obj(42)
-    o, lse = C.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, sd.device_tensor if p else None, 11)
+    amask = C.attn_mask(B, T, Hq, p, sd.device_tensor, 11, q) if p else None
+    o, lse = C.attn_fwd(q, k, v, amask, B, T, Hq, Hkv, scale, causal, p)
     ro, rlse = ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, sd, 11)
     close(lse, rlse, 2e-3, 1e-3, "lse")
     close(o, ro, 2e-2, 3e-2, "O")
@@ -189,8 +190,7 @@ def test_attention(B, T, Hq, Hkv, D, causal, p):
     dqkv = torch.empty_like(qkv)
     rdqkv = torch.empty_like(qkv)
     sl = lambda t: (t[:, :Hq * D], t[:, Hq * D:(Hq + Hkv) * D], t[:, (Hq + Hkv) * D:])
-    C.attn_bwd(q, k, v, o, do, lse, *sl(dqkv), B, T, Hq, Hkv, scale, causal, p,
-               sd.device_tensor if p else None, 11)
+    C.attn_bwd(q, k, v, o, do, lse, amask if p else None, *sl(dqkv), B, T, Hq, Hkv, scale, causal, p)
     ref.attn_bwd(q, k, v, o, do, lse, *sl(rdqkv), B, T, Hq, Hkv, scale, causal, p, sd, 11)
     for name, a, b in zip("qkv", sl(dqkv), sl(rdqkv)):
         close(a, b, 5e-2, 5e-2, "d" + name)
@@ -203,7 +203,8 @@ def test_attention_tinygpt_shape():
     qkv = rnd(B * T, 3 * H * D)
     q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
     sd = seed_obj(3)
-    o, lse = C.attn_fwd(q, k, v, B, T, H, H, 0.125, False, 0.1, sd.device_tensor, 1)
+    amask = C.attn_mask(B, T, H, 0.1, sd.device_tensor, 1, q)
+    o, lse = C.attn_fwd(q, k, v, amask, B, T, H, H, 0.125, False, 0.1)
     ro, rlse = ref.attn_fwd(q, k, v, B, T, H, H, 0.125, False, 0.1, sd, 1)
     close(o, ro, 2e-2, 3e-2, "O tier A")
 
