@@ -1,0 +1,124 @@
+"""Aggregate ``result.json`` files into ``metrics.csv`` (reference: scripts/parse_metrics.py:12-87).
+
+Output contract:
+
+* input: every file named exactly ``result.json`` below ``--results-dir`` (the collector layout
+  ``<job>_results/result.json``; the harness-side ``result_*.json`` names are NOT matched, as in the
+  reference);
+* rows sorted by ``[strategy, world_size, seq_len]``; columns = the 13 record keys in record order
+  plus ``scaling_efficiency_pct``;
+* ``scaling_efficiency_pct`` uses the reference formula per (strategy, seq_len) group with more than
+  one row: ``tps / (tps_of_first_row_at_min_ws * ws) * 100`` (single-row groups keep 100.0).  When
+  the smallest world size in a group is 2 this reads 50 % for the 2-GPU row — reproduced verbatim
+  for CSV compatibility.
+
+The corrected numbers go to ``metrics_extended.csv``: efficiency normalised to the group's WS=1 row
+(true weak-scaling efficiency), efficiency normalised to the smallest world size
+(``tps / (tps_min * ws / ws_min)``), per-GPU tokens/s, and the harness' extended sidecar fields when a
+``result.extended.json`` / ``result_*.extended.json`` sits next to the record.
+"""
+import argparse
+import json
+from pathlib import Path
+
+import pandas as pd
+
+SUMMARY_COLS = ["strategy", "world_size", "seq_len", "tier", "tokens_per_sec", "mean_step_time_sec",
+                "peak_vram_gb", "h2d_gbps_per_gpu", "scaling_efficiency_pct"]
+
+
+def load_records(results_dir):
+    root = Path(results_dir)
+    files = sorted(root.rglob("result.json"))
+    records, sources = [], []
+    for path in files:
+        try:
+            with open(path) as f:
+                records.append(json.load(f))
+            sources.append(path)
+        except Exception as e:  # noqa: BLE001 - a broken file must not stop the aggregation
+            print(f"WARNING: Failed to parse {path}: {e}")
+    return records, sources
+
+
+def reference_efficiency(df: pd.DataFrame) -> pd.Series:
+    eff = pd.Series(100.0, index=df.index)
+    for (_, _), grp in df.groupby(["strategy", "seq_len"], sort=False):
+        if len(grp) < 2:
+            continue
+        base = grp[grp["world_size"] == grp["world_size"].min()].iloc[0]["tokens_per_sec"]
+        for idx, row in grp.iterrows():
+            ideal = base * row["world_size"]
+            eff[idx] = (row["tokens_per_sec"] / ideal * 100.0) if ideal > 0 else 0.0
+    return eff
+
+
+def extended_frame(df: pd.DataFrame, sources) -> pd.DataFrame:
+    ext = df[["strategy", "world_size", "seq_len", "tier", "tokens_per_sec", "mean_step_time_sec",
+              "peak_vram_gb"]].copy()
+    ext["tokens_per_sec_per_gpu"] = ext["tokens_per_sec"] / ext["world_size"]
+    ext["efficiency_vs_ws1_pct"] = float("nan")
+    ext["efficiency_vs_min_ws_pct"] = float("nan")
+    for (_, _, _), grp in ext.groupby(["strategy", "seq_len", "tier"], sort=False):
+        ws_min = grp["world_size"].min()
+        base_min = grp[grp["world_size"] == ws_min].iloc[0]["tokens_per_sec"]
+        one = grp[grp["world_size"] == 1]
+        for idx, row in grp.iterrows():
+            ext.loc[idx, "efficiency_vs_min_ws_pct"] = row["tokens_per_sec"] / (base_min * row["world_size"] / ws_min) * 100.0
+            if len(one):
+                ext.loc[idx, "efficiency_vs_ws1_pct"] = row["tokens_per_sec"] / (one.iloc[0]["tokens_per_sec"] * row["world_size"]) * 100.0
+    # sidecar fields (harness extended records), matched by directory
+    extras = []
+    for src in sources:
+        cand = list(Path(src).parent.glob("*.extended.json"))
+        data = {}
+        if cand:
+            try:
+                with open(cand[0]) as f:
+                    e = json.load(f)
+                data = {k: e.get(k) for k in ("tflops_per_gpu", "mfu_vs_2.5PF_dense_bf16", "wall_time_timed_sec",
+                                               "comm_bytes_per_step_per_gpu", "peak_vram_reserved_gb",
+                                               "optimizer_steps", "engine", "accum_semantics")}
+            except Exception:
+                data = {}
+        extras.append(data)
+    if any(extras):
+        side = pd.DataFrame(extras, index=df.index)
+        ext = pd.concat([ext, side], axis=1)
+    return ext
+
+
+def parse_results(results_dir: str, output_dir: str):
+    out = Path(output_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    records, sources = load_records(results_dir)
+    if not records:
+        print(f"WARNING: No result.json files found in {results_dir}")
+        print("Expected files like: bench-master-*_results/result.json")
+        return None
+    print(f"Found {len(records)} result files")
+    df = pd.DataFrame(records)
+    order = df.sort_values(by=["strategy", "world_size", "seq_len"]).index
+    df = df.loc[order]
+    srcs = [sources[i] for i in order]
+    df["scaling_efficiency_pct"] = reference_efficiency(df)
+    csv = out / "metrics.csv"
+    df.to_csv(csv, index=False)
+    print(f"\nMetrics saved to: {csv}")
+    ext = extended_frame(df, srcs)
+    ext.to_csv(out / "metrics_extended.csv", index=False)
+    print("\n=== Summary ===")
+    print(df[SUMMARY_COLS].to_string(index=False))
+    return df
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Parse benchmark results to CSV")
+    ap.add_argument("--results-dir", required=True, help="Directory containing result JSON files")
+    ap.add_argument("--out", required=True, help="Output directory for metrics.csv")
+    a = ap.parse_args(argv)
+    parse_results(a.results_dir, a.out)
+
+
+if __name__ == "__main__":
+    main()

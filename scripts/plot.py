@@ -1,0 +1,11 @@
+#!/usr/bin/env python3
+"""CLI wrapper with the reference's path (scripts/plot.py); implementation: dltb.analysis.plot."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dltb.analysis.plot import main  # noqa: E402
+
+if __name__ == "__main__":
+    main()

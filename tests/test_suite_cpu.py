@@ -1,0 +1,38 @@
+"""End-to-end suite rehearsal on CPU/gloo (BASELINE.json config #1): torchrun launcher -> harness ->
+collector -> parse_metrics -> plot -> make_report, including the failure path."""
+import json
+import os
+import subprocess
+
+import pandas as pd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _suite(tmp_path, extra, strats="ddp zero2"):
+    env = dict(os.environ, STEPS="6", SEQ="64", TIER="tiny", WS_LIST="1 2", STRATS=strats, FORCE_NPROC="2",
+               HARNESS_EXTRA=f"--device cpu --warmup-steps 2 --log-every 0 {extra}", TIMEOUT="300",
+               OMP_NUM_THREADS="1")
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "run_all_benchmarks.sh"), str(tmp_path)],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r
+
+
+def test_suite_ddp_zero2_world_1_and_2(tmp_path):
+    _suite(tmp_path, "")
+    df = pd.read_csv(tmp_path / "summary" / "metrics.csv")
+    assert sorted(zip(df.strategy, df.world_size)) == [("ddp", 1), ("ddp", 2), ("zero2", 1), ("zero2", 2)]
+    assert (df.loc[df.world_size == 1, "scaling_efficiency_pct"] == 100.0).all()
+    assert (tmp_path / "summary" / "BENCHMARK_REPORT.md").exists()
+    assert (tmp_path / "summary" / "plots" / "tokens_per_sec_vs_gpu.png").exists()
+    assert json.load(open(tmp_path / "summary" / "failures.json")) == {"failed": []}
+    ext = pd.read_csv(tmp_path / "summary" / "metrics_extended.csv")
+    assert "efficiency_vs_ws1_pct" in ext.columns and ext["efficiency_vs_ws1_pct"].notna().all()
+    assert (tmp_path / "bench-master-ddp-ws2-seq64_results" / "result.extended.json").exists()
+
+
+def test_suite_records_failures_and_still_exits_zero(tmp_path):
+    _suite(tmp_path, "--fail-at-step 3", strats="ddp")
+    failed = json.load(open(tmp_path / "summary" / "failures.json"))["failed"]
+    assert failed == ["bench-master-ddp-ws1-seq64", "bench-master-ddp-ws2-seq64"]
