@@ -32,6 +32,13 @@ BASELINES = {"ddp": {2: 8369.4557, 4: 12220.3415}, "fsdp": {2: 6771.0, 4: 9424.0
              "zero2": {2: 10999.0, 4: 18147.0}, "zero3": {2: 10560.0, 4: 15977.0}}
 
 
+def _model_name(tier, c):
+    if c.arch == "mistral":
+        return (f"Mistral-7B-shape ({c.num_params() / 1e9:.2f}B params, d{c.n_embd}/h{c.n_head}/kv{c.kv_heads}/"
+                f"L{c.n_layer}, ffn {c.ffn_dim}, vocab {c.vocab_size})")
+    return f"TinyGPT-{tier} ({c.num_params() / 1e6:.1f}M params, d{c.n_embd}/h{c.n_head}/L{c.n_layer}, vocab {c.vocab_size})"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -67,7 +74,8 @@ def main():
     tmode = setup_tunableop(args.tunableop if (args.tunableop != "tune" or rank == 0) else "use")
     torch.manual_seed(42)
     mcfg = get_model_config(args.tier, args.seq_len)
-    model = build_model(mcfg)
+    with torch.device(device):          # random init straight into HBM (7B-class models never touch host RAM)
+        model = build_model(mcfg)
     h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None,
                            grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype="bf16",
                            bucket_mb=args.bucket_mb, seed=42)
@@ -118,11 +126,10 @@ def main():
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": value / BASELINE_TPS,
+            "vs_baseline": value / BASELINE_TPS if (args.tier == "A" and args.seq_len == 2048) else None,
             "dtype": "bf16",
             "data": "synthetic",
-            "config": {"model": f"TinyGPT-{args.tier} ({mcfg.num_params() / 1e6:.1f}M params, d{mcfg.n_embd}/"
-                                f"h{mcfg.n_head}/L{mcfg.n_layer}, vocab {mcfg.vocab_size})",
+            "config": {"model": _model_name(args.tier, mcfg),
                        "global_batch": args.per_device_batch * accum * world,
                        "micro_batch_per_gpu": args.per_device_batch,
                        "grad_accum": accum,

@@ -47,7 +47,7 @@ def build_parser():
     p.add_argument("--master-addr", type=str, default=None)
     p.add_argument("--master-port", type=int, default=None)
     # model & data
-    p.add_argument("--tier", type=str, required=True, choices=["A", "B", "default", "M7B", "tiny"])
+    p.add_argument("--tier", type=str, required=True, choices=["A", "B", "default", "M7B", "tiny", "mtiny"])
     p.add_argument("--seq-len", type=int, required=True)
     p.add_argument("--synthetic", action="store_true", help="accepted for compatibility (data is always synthetic)")
     # training
@@ -116,7 +116,8 @@ def train(args):
         mcfg = get_model_config(args.tier, args.seq_len)
         if args.dropout is not None:
             mcfg.dropout = args.dropout
-        model = build_model(mcfg)
+        with torch.device(device):      # init directly on the GPU (no fp32 host copy of a 7B model)
+            model = build_model(mcfg)
         n_params = model.num_params()
         if is_main:
             print(f"Model initialized: {n_params / 1e6:.2f}M parameters", flush=True)

@@ -75,7 +75,7 @@ class ModelConfig:
         return 6.0 * n_mat + attn
 
 
-TIERS = ("A", "B", "default", "M7B", "tiny")
+TIERS = ("A", "B", "default", "M7B", "tiny", "mtiny")
 
 
 def get_model_config(tier: str, seq_len: int, dropout: float = 0.1) -> ModelConfig:
@@ -96,4 +96,8 @@ def get_model_config(tier: str, seq_len: int, dropout: float = 0.1) -> ModelConf
     if tier == "tiny":   # unit-test shape (CPU friendly)
         return ModelConfig(vocab_size=128, n_embd=64, n_head=4, n_layer=2, block_size=seq_len,
                            dropout=dropout, tier="tiny")
+    if tier == "mtiny":  # Mistral-shape unit-test model: GQA 2:1, head_dim 64 (the GPU attention's smallest)
+        return ModelConfig(arch="mistral", vocab_size=256, n_embd=128, n_head=2, n_kv_head=1, n_layer=2,
+                           ffn_hidden=256, block_size=seq_len, dropout=0.0, causal=True,
+                           tie_embeddings=False, rope_theta=10000.0, tier="mtiny")
     raise ValueError(f"Unknown tier: {tier}")

@@ -138,7 +138,7 @@ def rope_tables(T, D, theta, device=None):
 def rope_(qkv2d, cos, sin, T, heads, D, inverse=False):
     N = qkv2d.shape[0]
     half = D // 2
-    x = qkv2d[:, :heads * D].float().view(N // T, T, heads, D)
+    x = _f(qkv2d[:, :heads * D]).view(N // T, T, heads, D)
     x1, x2 = x[..., :half], x[..., half:]
     c = cos[:T].view(1, T, 1, half)
     s = sin[:T].view(1, T, 1, half)
