@@ -179,15 +179,73 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ m
 }
 
 // =============================================================================== forward
-template <int D, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
+// Workgroup = KS key-splits x 4 waves; wave (qw, sp) owns query rows q0 .. q0+31 and the key tiles
+// t == sp (mod KS).  KS = 2 doubles the waves per query block (2 waves / SIMD even at B*Hq*T/128
+// = 256 workgroups, TinyGPT-A's shape); the two partial (m, l, O) states merge through LDS.
+// Online softmax with a lazy rescale: the running max m only moves (and O, l are rescaled) when a
+// tile's row max exceeds m by more than kRescaleLog2 (p <= 2^8, safe in f32 and bf16); the decision
+// is wave-uniform so the rescale is a branch, not per-tile work.  The causal mask is applied on
+// diagonal tiles only.  Dropout: p & sbfe(keep_word, bit) (2 VALU per probability).
+constexpr float kRescaleLog2 = 8.f;
+
+template <int I>
+struct IC { static constexpr int value = I; constexpr operator int() const { return I; } };
+template <int N, int I = 0, typename F>
+DLTB_DEV void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(IC<I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <int D>
+DLTB_DEV bfx8 pack_frag(const f32x16& x, int s) {      // regs 8s .. 8s+7 -> bf16 B operand
+  typedef __bf16 bfx2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  bfx8 f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x2 p = {x[8 * s + 2 * j], x[8 * s + 2 * j + 1]};
+    const bfx2 b = __builtin_convertvector(p, bfx2);
+    f[2 * j] = b[0];
+    f[2 * j + 1] = b[1];
+  }
+  return f;
+}
+
+template <int BIT>
+DLTB_DEV float keep_and(float p, uint32_t mw) {
+  // sign-extended 1-bit field -> 0 / ~0 mask; asm keeps the compiler from re-forming and+cmp+cndmask
+  uint32_t k;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(mw), "n"(BIT));
+  return __uint_as_float(__float_as_uint(p) & k);
+}
+
+// XCD-aware block order: consecutive workgroup ids land on different XCDs (round robin over 8),
+// so walk the (head, query block) space with the XCD index as the slowest digit -> the query
+// blocks of one head share an XCD's L2 for their K/V stream.  Causal grids visit the heaviest
+// (last) query blocks first.
+DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
+  const int L = blockIdx.x, total = nqb * nbh;
+  int idx = L;
+  if ((total & 7) == 0) idx = (L & 7) * (total >> 3) + (L >> 3);
+  bh = idx / nqb;
+  qb = idx % nqb;
+  if (causal) qb = nqb - 1 - qb;
+}
+
+template <int D, bool CAUSAL, bool DROP, int KS>
+__global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
+  constexpr int NACC = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
-  const int T = P.T;
-  const int nT = T / kTile;
-  const int q0 = blockIdx.x * kBlockRows + w * 32;
+  const int qw = w & 3, sp = w >> 2, stid = tid & 255;
+  const int T = P.T, nT = T / kTile;
+  int qb, bh;
+  block_coords(T / kBlockRows, P.B * P.Hq, CAUSAL, qb, bh);
+  const int b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
+  const int q0 = qb * kBlockRows + qw * 32;
   const int qi = q0 + r;
 
   bfx8 qf[D / 16];
@@ -196,37 +254,41 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) qf[s] = __builtin_bit_cast(bfx8, ld16<uint4>(qrow + 16 * s + 8 * h));
   }
-  int nt = nT;
-  if (CAUSAL) nt = min(nt, (blockIdx.x * kBlockRows + kBlockRows - 1) / kTile + 1);
+  const int nt = CAUSAL ? min(nT, (qb * kBlockRows + kBlockRows - 1) / kTile + 1) : nT;
+  const int nit = (nt + KS - 1) / KS;
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
   const uint32_t* mrow = DROP ? P.mask + ((long)bh * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
 
   TileLoader<D> lk, lv;
-  lk.load(kbase, P.k_stride, 0, tid);
-  lv.load(vbase, P.v_stride, 0, tid);
-  uint32_t mw_next = DROP ? mrow[0] : 0u;
-  lk.store(smem, tid);
-  lv.store(smem + TB, tid);
+  if (sp < nt) {
+    lk.load(kbase, P.k_stride, sp * kTile, stid);
+    lv.load(vbase, P.v_stride, sp * kTile, stid);
+    lk.store(smem + sp * 2 * TB, stid);
+    lv.store(smem + sp * 2 * TB + TB, stid);
+  }
+  uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
   __syncthreads();
 
-  f32x16 oacc[D / 32];
+  f32x16 oacc[NACC];
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt) oacc[dt] = f32x16{};
+  for (int dt = 0; dt < NACC; ++dt) oacc[dt] = f32x16{};
   float m = -INFINITY, l = 0.f;   // m in scaled log2 units
 
-  for (int t = 0; t < nt; ++t) {
-    const char* kt = smem + (t & 1) * 2 * TB;
+  for (int it = 0; it < nit; ++it) {
+    const int t = it * KS + sp;
+    const char* kt = smem + ((it & 1) * KS + sp) * 2 * TB;
     const char* vt = kt + TB;
     const uint32_t mw = mw_next;
-    if (t + 1 < nt) {
-      lk.load(kbase, P.k_stride, (t + 1) * kTile, tid);
-      lv.load(vbase, P.v_stride, (t + 1) * kTile, tid);
-      if (DROP) mw_next = mrow[(long)(t + 1) * 2 * T];
+    const int tn = t + KS;
+    if (tn < nt) {
+      lk.load(kbase, P.k_stride, tn * kTile, stid);
+      lv.load(vbase, P.v_stride, tn * kTile, stid);
+      if (DROP) mw_next = mrow[(long)tn * 2 * T];
     }
     const int kv0 = t * kTile;
-    if (!CAUSAL || kv0 <= q0 + 31) {
+    if (t < nt && (!CAUSAL || kv0 <= q0 + 31)) {
       f32x16 sacc[2];
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
@@ -234,52 +296,75 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
 #pragma unroll
         for (int s = 0; s < D / 16; ++s) sacc[n] = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sacc[n]);
       }
-      float mx = -INFINITY;
+      if (CAUSAL && kv0 + kTile - 1 > q0) {        // diagonal tile: mask keys > query
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) sacc[n][i] = -INFINITY;
+      }
+      float mx = sacc[0][0];
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float v = sacc[n][i];
-          if (CAUSAL) {
-            const int key = kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (key > qi) v = -INFINITY;
-            sacc[n][i] = v;
-          }
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx * c);
-      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-      m = mnew;
+        for (int i = (n == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, sacc[n][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
+      if (__ballot(mx > m + kRescaleLog2)) {         // wave-uniform, rare after the first tiles
+        const float mnew = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
+      }
       float ls = 0.f;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(sacc[n][i], c, -mnew));
-          ls += p;
-          sacc[n][i] = (!DROP || ((mw >> (16 * n + i)) & 1u)) ? p : 0.f;
-        }
-      l = l * alpha + ls;
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) oacc[dt] *= alpha;
+      static_for<32>([&](auto I) {
+        constexpr int n = I / 16, i = I % 16;
+        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[n][i], c, -m));
+        ls += p;
+        sacc[n][i] = DROP ? keep_and<I>(p, mw) : p;
+      });
+      l += ls;
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bfx8 pf = acc_to_frag(sacc[n], s2);
+          const bfx8 pf = pack_frag<D>(sacc[n], s2);
 #pragma unroll
-          for (int dt = 0; dt < D / 32; ++dt)
+          for (int dt = 0; dt < NACC; ++dt)
             oacc[dt] = mfma32(tr_frag<D>(vt, 32 * n + 16 * s2, dt * 32, lane), pf, oacc[dt]);
         }
       }
     }
-    if (t + 1 < nt) {
-      char* nk = smem + ((t + 1) & 1) * 2 * TB;
-      lk.store(nk, tid);
-      lv.store(nk + TB, tid);
+    if (tn < nt) {
+      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
+      lk.store(nk, stid);
+      lv.store(nk + TB, stid);
     }
     __syncthreads();
+  }
+  if constexpr (KS == 2) {     // merge the two key halves: split 1 -> LDS -> split 0
+    constexpr int NF = 16 * NACC + 2;
+    float* red = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
+    if (sp == 1) {
+      red[0] = m;
+      red[64] = l;
+#pragma unroll
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(2 + 16 * dt + i) * 64] = oacc[dt][i];
+    }
+    __syncthreads();
+    if (sp == 1) return;
+    const float m1 = red[0], l1 = red[64];
+    const float mn = fmaxf(m, m1);
+    const float a0 = __builtin_amdgcn_exp2f(m - mn), a1 = __builtin_amdgcn_exp2f(m1 - mn);
+    m = mn;
+    l = l * a0 + l1 * a1;
+#pragma unroll
+    for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] = oacc[dt][i] * a0 + red[(2 + 16 * dt + i) * 64] * a1;
   }
   l += __shfl_xor(l, 32, 64);
   const float inv = (DROP ? P.drop_scale : 1.f) / l;
@@ -287,6 +372,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs P) {
   store_acc_rows<D>(orow, oacc, inv, h);
   if (h == 0) P.lse[((long)b * P.Hq + hq) * T + qi] = (m + __log2f(l)) * 0.69314718055994531f;
 }
+
+template <int D>
+constexpr int fwd_ks() { return 2; }
+template <int D>
+constexpr int fwd_smem_bytes() { return 4 * fwd_ks<D>() * kTile * D * 2; }
 
 // =============================================================================== backward prep
 // delta[b, h, t] = sum_d dO[b,t,h,d] * O[b,t,h,d]
@@ -318,28 +408,55 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs P) {
 }
 
 // =============================================================================== dK / dV
+// Workgroup = KS query-splits x 4 waves; wave (kw, sp) owns keys k0 .. k0+31 (K, V in registers)
+// and sweeps the query tiles t == sp (mod KS) of every query head of its KV group.  The two
+// partial dK/dV accumulators merge through LDS at the end.  Dropout folds into
+//   pd = p & keep,  ds' = p * ((dp & keep) - delta / s)     (s = 1/(1-p); dK, dV scaled by s at the store)
+// so each probability costs bfe + 2 and + sub + mul besides its exp.
+template <int D>
+constexpr int dkdv_ks() { return D == 64 ? 2 : 1; }
+template <int D>
+constexpr int dkdv_stage_bytes() { return 2 * kTile * D * 2 + 2 * kTile * 4 + kTile * 16; }
 template <int D>
 constexpr int dkdv_smem_bytes() {
-  return 2 * (2 * kTile * D * 2 + 2 * kTile * 4 + kTile * 16);
+  constexpr int a = 2 * dkdv_ks<D>() * dkdv_stage_bytes<D>();
+  constexpr int merge = 4 * 64 * 4 * (2 * 16 * (D / 32));
+  return dkdv_ks<D>() == 2 && merge > a ? merge : a;
 }
 
-template <int D, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
+DLTB_DEV float keep_and_v(float p, uint32_t mw, uint32_t bit) {
+  uint32_t k;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(mw), "v"(bit));
+  return __uint_as_float(__float_as_uint(p) & k);
+}
+DLTB_DEV uint32_t keep_mask_v(uint32_t mw, uint32_t bit) {
+  uint32_t k;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(mw), "v"(bit));
+  return k;
+}
+
+template <int D, bool CAUSAL, bool DROP, int KS>
+__global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
-  constexpr int SB = dkdv_smem_bytes<D>() / 2;   // Q tile, dO tile, lse2[64], delta[64], mask[64][4]
+  constexpr int SB = dkdv_stage_bytes<D>();   // Q tile, dO tile, lse2[64], delta'[64], mask[64][4]
+  constexpr int NACC = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int bk = blockIdx.y, b = bk / P.Hkv, hk = bk % P.Hkv;
+  const int kw = w & 3, sp = w >> 2, stid = tid & 255;
+  const int T = P.T, nT = T / kTile;
+  int kb, bk;
+  block_coords(T / kBlockRows, P.B * P.Hkv, false, kb, bk);
+  if (CAUSAL) kb = T / kBlockRows - 1 - kb;      // heaviest key blocks (first keys) ... last
+  const int b = bk / P.Hkv, hk = bk % P.Hkv;
   const int G = P.Hq / P.Hkv;
-  const int T = P.T;
-  const int nT = T / kTile;
-  const int kblk0 = blockIdx.x * kBlockRows;
-  const int k0 = kblk0 + w * 32;
+  const int kblk0 = kb * kBlockRows;
+  const int k0 = kblk0 + kw * 32;
   const int key = k0 + r;
   // this lane's bit in the packed mask words (see attn_mask_kernel)
   const int hbit = (r >> 2) & 1;
-  const int jbit = 16 * (w & 1) + ((r & 3) | (((r >> 3) & 3) << 2));
-  const int msub = (w >> 1) * 2 + hbit;
+  const uint32_t jbit = 16 * (kw & 1) + ((r & 3) | (((r >> 3) & 3) << 2));
+  const int msub = (kw >> 1) * 2 + hbit;
+  const float inv_s = DROP ? 1.f / P.drop_scale : 1.f;
 
   bfx8 kf[D / 16], vf[D / 16];
   {
@@ -351,58 +468,63 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
       vf[s] = __builtin_bit_cast(bfx8, ld16<uint4>(vrow + 16 * s + 8 * h));
     }
   }
-  f32x16 dk[D / 32], dv[D / 32];
+  f32x16 dk[NACC], dv[NACC];
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt) { dk[dt] = f32x16{}; dv[dt] = f32x16{}; }
+  for (int dt = 0; dt < NACC; ++dt) { dk[dt] = f32x16{}; dv[dt] = f32x16{}; }
 
   const float c = P.scale * kLog2e;
   const int t_begin = CAUSAL ? kblk0 / kTile : 0;
+  const int nit = (nT - t_begin + KS - 1) / KS;   // iterations per head
+  const int njobs = G * nit;
 
-  for (int g = 0; g < G; ++g) {
+  TileLoader<D> lq, ldo;
+  float vl = 0.f, vd = 0.f;
+  uint32_t mword = 0;
+  auto tile_of = [&](int j, int& g, int& t) { g = j / nit; t = t_begin + (j % nit) * KS + sp; };
+  auto load = [&](int j) {
+    int g, t;
+    tile_of(j, g, t);
+    if (t >= nT) return;
     const int hq = hk * G + g;
     const long bq = (long)b * P.Hq + hq;
-    const bf16_t* qbase = P.q + (long)b * T * P.q_stride + hq * D;
-    const bf16_t* dobase = P.dout + (long)b * T * P.do_stride + hq * D;
-    TileLoader<D> lq, ldo;
-    float vl = 0.f, vd = 0.f;
-    uint32_t mword = 0;
-    auto load_small = [&](int t) {
-      if (tid < kTile) {
-        vl = P.lse[bq * T + t * kTile + tid] * kLog2e;
-        vd = P.delta[bq * T + t * kTile + tid];
-      }
-      if (DROP) {
-        const int row = tid >> 2, sb = tid & 3;
-        mword = P.mask[((bq * nT + (blockIdx.x * 2 + (sb >> 1))) * 2 + (sb & 1)) * T + t * kTile + row];
-      }
-    };
-    auto store_small = [&](char* base) {
-      float* f = reinterpret_cast<float*>(base + 2 * TB);
-      if (tid < kTile) {
-        f[tid] = vl;
-        f[kTile + tid] = vd;
-      }
-      if (DROP) reinterpret_cast<uint32_t*>(f + 2 * kTile)[tid] = mword;
-    };
-    lq.load(qbase, P.q_stride, t_begin * kTile, tid);
-    ldo.load(dobase, P.do_stride, t_begin * kTile, tid);
-    load_small(t_begin);
-    lq.store(smem, tid);
-    ldo.store(smem + TB, tid);
-    store_small(smem);
-    __syncthreads();
-    for (int t = t_begin; t < nT; ++t) {
-      const int bufi = (t - t_begin) & 1;
-      const char* qt = smem + bufi * SB;
-      const char* dt_ = qt + TB;
-      const float* lse2 = reinterpret_cast<const float*>(qt + 2 * TB);
-      const float* dlt = lse2 + kTile;
-      const uint32_t* mws = reinterpret_cast<const uint32_t*>(dlt + kTile);
-      if (t + 1 < nT) {
-        lq.load(qbase, P.q_stride, (t + 1) * kTile, tid);
-        ldo.load(dobase, P.do_stride, (t + 1) * kTile, tid);
-        load_small(t + 1);
-      }
+    lq.load(P.q + (long)b * T * P.q_stride + hq * D, P.q_stride, t * kTile, stid);
+    ldo.load(P.dout + (long)b * T * P.do_stride + hq * D, P.do_stride, t * kTile, stid);
+    if (stid < kTile) {
+      vl = P.lse[bq * T + t * kTile + stid] * kLog2e;
+      vd = P.delta[bq * T + t * kTile + stid] * inv_s;
+    }
+    if (DROP) {
+      const int row = stid >> 2, sb = stid & 3;
+      mword = P.mask[((bq * nT + (kb * 2 + (sb >> 1))) * 2 + (sb & 1)) * T + t * kTile + row];
+    }
+  };
+  auto store = [&](int j) {
+    int g, t;
+    tile_of(j, g, t);
+    if (t >= nT) return;
+    char* base = smem + ((j & 1) * KS + sp) * SB;
+    lq.store(base, stid);
+    ldo.store(base + TB, stid);
+    float* f = reinterpret_cast<float*>(base + 2 * TB);
+    if (stid < kTile) {
+      f[stid] = vl;
+      f[kTile + stid] = vd;
+    }
+    if (DROP) reinterpret_cast<uint32_t*>(f + 2 * kTile)[stid] = mword;
+  };
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int j = 0; j < njobs; ++j) {
+    int g_, t;
+    tile_of(j, g_, t);
+    const char* qt = smem + ((j & 1) * KS + sp) * SB;
+    const char* dt_ = qt + TB;
+    const float* lse2 = reinterpret_cast<const float*>(qt + 2 * TB);
+    const float* dlt = lse2 + kTile;
+    const uint32_t* mws = reinterpret_cast<const uint32_t*>(dlt + kTile);
+    if (j + 1 < njobs) load(j + 1);
+    if (t < nT) {
 #pragma unroll
       for (int mm = 0; mm < 2; ++mm) {
         const int qb = t * kTile + 32 * mm;
@@ -413,6 +535,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
           sa = mfma32(row_frag<D>(qt, 32 * mm + r, 2 * s + h), kf[s], sa);
           dp = mfma32(row_frag<D>(dt_, 32 * mm + r, 2 * s + h), vf[s], dp);
         }
+        const bool diag = CAUSAL && qb < k0 + 31;
         f32x16 pd, ds;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -425,11 +548,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
           for (int e = 0; e < 4; ++e) {
             const int i = 4 * g4 + e;
             float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
-            if (CAUSAL && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
+            if (diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
             if (DROP) {
-              const bool keep = (mws[(ql + e) * 4 + msub] >> jbit) & 1u;
-              pd[i] = keep ? p : 0.f;
-              ds[i] = p * ((keep ? dp[i] * P.drop_scale : 0.f) - Dv[e]);
+              const uint32_t km = keep_mask_v(mws[(ql + e) * 4 + msub], jbit);
+              pd[i] = __uint_as_float(__float_as_uint(p) & km);
+              ds[i] = p * (__uint_as_float(__float_as_uint(dp[i]) & km) - Dv[e]);
             } else {
               pd[i] = p;
               ds[i] = p * (dp[i] - Dv[e]);
@@ -438,40 +561,67 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnArgs P) {
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const bfx8 pf = acc_to_frag(pd, s2);
-          const bfx8 sf = acc_to_frag(ds, s2);
+          const bfx8 pf = pack_frag<D>(pd, s2);
+          const bfx8 sf = pack_frag<D>(ds, s2);
 #pragma unroll
-          for (int d_ = 0; d_ < D / 32; ++d_) {
+          for (int d_ = 0; d_ < NACC; ++d_) {
             dv[d_] = mfma32(tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane), pf, dv[d_]);
             dk[d_] = mfma32(tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane), sf, dk[d_]);
           }
         }
       }
-      if (t + 1 < nT) {
-        char* nb = smem + ((t + 1 - t_begin) & 1) * SB;
-        lq.store(nb, tid);
-        ldo.store(nb + TB, tid);
-        store_small(nb);
-      }
-      __syncthreads();
     }
+    if (j + 1 < njobs) store(j + 1);
+    __syncthreads();
   }
+  if constexpr (KS == 2) {
+    constexpr int NF = 2 * 16 * NACC;
+    float* red = reinterpret_cast<float*>(smem) + kw * NF * 64 + lane;
+    if (sp == 1) {
+#pragma unroll
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          red[(16 * dt + i) * 64] = dk[dt][i];
+          red[(16 * (NACC + dt) + i) * 64] = dv[dt][i];
+        }
+    }
+    __syncthreads();
+    if (sp == 1) return;
+#pragma unroll
+    for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        dk[dt][i] += red[(16 * dt + i) * 64];
+        dv[dt][i] += red[(16 * (NACC + dt) + i) * 64];
+      }
+  }
+  const float s_drop = DROP ? P.drop_scale : 1.f;
   bf16_t* dkrow = P.out + ((long)b * T + key) * P.out_stride + hk * D;
   bf16_t* dvrow = P.out2 + ((long)b * T + key) * P.out2_stride + hk * D;
-  store_acc_rows<D>(dkrow, dk, P.scale, h);
-  store_acc_rows<D>(dvrow, dv, DROP ? P.drop_scale : 1.f, h);
+  store_acc_rows<D>(dkrow, dk, P.scale * s_drop, h);
+  store_acc_rows<D>(dvrow, dv, s_drop, h);
 }
 
 // =============================================================================== dQ
-template <int D, bool CAUSAL, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs P) {
+// Query-major, KS key-splits per workgroup as in the forward; dQ partials merge through LDS.
+template <int D>
+constexpr int dq_ks() { return 2; }
+template <int D>
+constexpr int dq_smem_bytes() { return 4 * dq_ks<D>() * kTile * D * 2; }
+
+template <int D, bool CAUSAL, bool DROP, int KS>
+__global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
+  constexpr int NACC = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
-  const int T = P.T;
-  const int nT = T / kTile;
-  const int q0 = blockIdx.x * kBlockRows + w * 32;
+  const int qw = w & 3, sp = w >> 2, stid = tid & 255;
+  const int T = P.T, nT = T / kTile;
+  int qb, bh;
+  block_coords(T / kBlockRows, P.B * P.Hq, CAUSAL, qb, bh);
+  const int b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
+  const int q0 = qb * kBlockRows + qw * 32;
   const int qi = q0 + r;
   const long bq = (long)b * P.Hq + hq;
 
@@ -486,71 +636,93 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs P) {
     }
   }
   const float lse2 = P.lse[bq * T + qi] * kLog2e;
-  const float dl = P.delta[bq * T + qi];
+  const float dl = P.delta[bq * T + qi] * (DROP ? 1.f / P.drop_scale : 1.f);
   const uint32_t* mrow = DROP ? P.mask + ((long)bq * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
-  int nt = nT;
-  if (CAUSAL) nt = min(nt, (blockIdx.x * kBlockRows + kBlockRows - 1) / kTile + 1);
+  const int nt = CAUSAL ? min(nT, (qb * kBlockRows + kBlockRows - 1) / kTile + 1) : nT;
+  const int nit = (nt + KS - 1) / KS;
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
 
   TileLoader<D> lk, lv;
-  lk.load(kbase, P.k_stride, 0, tid);
-  lv.load(vbase, P.v_stride, 0, tid);
-  uint32_t mw_next = DROP ? mrow[0] : 0u;
-  lk.store(smem, tid);
-  lv.store(smem + TB, tid);
+  if (sp < nt) {
+    lk.load(kbase, P.k_stride, sp * kTile, stid);
+    lv.load(vbase, P.v_stride, sp * kTile, stid);
+    lk.store(smem + sp * 2 * TB, stid);
+    lv.store(smem + sp * 2 * TB + TB, stid);
+  }
+  uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
   __syncthreads();
 
-  f32x16 dq[D / 32];
+  f32x16 dq[NACC];
 #pragma unroll
-  for (int dt = 0; dt < D / 32; ++dt) dq[dt] = f32x16{};
+  for (int dt = 0; dt < NACC; ++dt) dq[dt] = f32x16{};
 
-  for (int t = 0; t < nt; ++t) {
-    const char* kt = smem + (t & 1) * 2 * TB;
+  for (int it = 0; it < nit; ++it) {
+    const int t = it * KS + sp;
+    const char* kt = smem + ((it & 1) * KS + sp) * 2 * TB;
     const char* vt = kt + TB;
     const uint32_t mw = mw_next;
-    if (t + 1 < nt) {
-      lk.load(kbase, P.k_stride, (t + 1) * kTile, tid);
-      lv.load(vbase, P.v_stride, (t + 1) * kTile, tid);
-      if (DROP) mw_next = mrow[(long)(t + 1) * 2 * T];
+    const int tn = t + KS;
+    if (tn < nt) {
+      lk.load(kbase, P.k_stride, tn * kTile, stid);
+      lv.load(vbase, P.v_stride, tn * kTile, stid);
+      if (DROP) mw_next = mrow[(long)tn * 2 * T];
     }
     const int kv0 = t * kTile;
+    if (t < nt) {
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      if (CAUSAL && kv0 + 32 * n > q0 + 31) continue;
-      f32x16 sa = f32x16{}, dp = f32x16{};
+      for (int n = 0; n < 2; ++n) {
+        if (CAUSAL && kv0 + 32 * n > q0 + 31) continue;
+        f32x16 sa = f32x16{}, dp = f32x16{};
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        sa = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sa);
-        dp = mfma32(row_frag<D>(vt, 32 * n + r, 2 * s + h), of[s], dp);
-      }
-      f32x16 ds;
+        for (int s = 0; s < D / 16; ++s) {
+          sa = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sa);
+          dp = mfma32(row_frag<D>(vt, 32 * n + r, 2 * s + h), of[s], dp);
+        }
+        const bool diag = CAUSAL && kv0 + 32 * n + 31 > q0;
+        f32x16 ds;
+        static_for<16>([&](auto I) {
+          constexpr int i = I;
+          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -lse2));
+          if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
+          const float dpv = DROP ? (n == 0 ? keep_and<I>(dp[i], mw) : keep_and<16 + I>(dp[i], mw)) : dp[i];
+          ds[i] = p * (dpv - dl);
+        });
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -lse2));
-        if (CAUSAL && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
-        float dpv = dp[i];
-        if (DROP) dpv = ((mw >> (16 * n + i)) & 1u) ? dpv * P.drop_scale : 0.f;
-        ds[i] = p * (dpv - dl);
-      }
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bfx8 sf = pack_frag<D>(ds, s2);
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bfx8 sf = acc_to_frag(ds, s2);
-#pragma unroll
-        for (int dt = 0; dt < D / 32; ++dt)
-          dq[dt] = mfma32(tr_frag<D>(kt, 32 * n + 16 * s2, dt * 32, lane), sf, dq[dt]);
+          for (int dt = 0; dt < NACC; ++dt)
+            dq[dt] = mfma32(tr_frag<D>(kt, 32 * n + 16 * s2, dt * 32, lane), sf, dq[dt]);
+        }
       }
     }
-    if (t + 1 < nt) {
-      char* nk = smem + ((t + 1) & 1) * 2 * TB;
-      lk.store(nk, tid);
-      lv.store(nk + TB, tid);
+    if (tn < nt) {
+      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
+      lk.store(nk, stid);
+      lv.store(nk + TB, stid);
     }
     __syncthreads();
   }
+  if constexpr (KS == 2) {
+    constexpr int NF = 16 * NACC;
+    float* red = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
+    if (sp == 1) {
+#pragma unroll
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[(16 * dt + i) * 64] = dq[dt][i];
+    }
+    __syncthreads();
+    if (sp == 1) return;
+#pragma unroll
+    for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) dq[dt][i] += red[(16 * dt + i) * 64];
+  }
   bf16_t* dqrow = P.out + ((long)b * T + qi) * P.out_stride + hq * D;
-  store_acc_rows<D>(dqrow, dq, P.scale, h);
+  store_acc_rows<D>(dqrow, dq, P.scale * (DROP ? P.drop_scale : 1.f), h);
 }
 
 AttnArgs make_args(const void* q, const void* k, const void* v, long qs, long ks, long vs, int B,
@@ -586,26 +758,19 @@ namespace {
 
 template <int D, bool C, bool DR>
 void set_attrs() {
-  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, C, DR>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTile * D * 2);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kTile * D * 2);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, C, DR>,
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, C, DR, fwd_ks<D>()>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, fwd_smem_bytes<D>());
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR, dq_ks<D>()>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, dq_smem_bytes<D>());
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, C, DR, dkdv_ks<D>()>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, dkdv_smem_bytes<D>());
 }
 
 template <int D, bool C, bool DR>
 void launch_fwd(const AttnArgs& a, hipStream_t st) {
-  dim3 grid(a.T / kBlockRows, a.B * a.Hq);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, C, DR>), grid, dim3(256), 4 * kTile * D * 2, st, a);
-}
-
-template <int D, bool C, bool DR>
-void launch_bwd(const AttnArgs& a, const AttnArgs& kv, hipStream_t st) {
-  dim3 gkv(a.T / kBlockRows, a.B * a.Hkv);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR>), gkv, dim3(256), dkdv_smem_bytes<D>(), st, kv);
-  dim3 gq(a.T / kBlockRows, a.B * a.Hq);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR>), gq, dim3(256), 4 * kTile * D * 2, st, a);
+  constexpr int KS = fwd_ks<D>();
+  dim3 grid((a.T / kBlockRows) * a.B * a.Hq);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, C, DR, KS>), grid, dim3(256 * KS), fwd_smem_bytes<D>(), st, a);
 }
 
 #define DLTB_ATTN_DISPATCH(FN, D, C, DR, ...)           \
@@ -677,13 +842,15 @@ void dltb_attn_bwd_delta(const void* o, const void* dout, float* delta, long os,
 namespace {
 template <int D, bool C, bool DR>
 void launch_dkdv(const AttnArgs& a, hipStream_t st) {
-  dim3 gkv(a.T / kBlockRows, a.B * a.Hkv);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR>), gkv, dim3(256), dkdv_smem_bytes<D>(), st, a);
+  constexpr int KS = dkdv_ks<D>();
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hkv), dim3(256 * KS),
+                     dkdv_smem_bytes<D>(), st, a);
 }
 template <int D, bool C, bool DR>
 void launch_dq(const AttnArgs& a, hipStream_t st) {
-  dim3 gq(a.T / kBlockRows, a.B * a.Hq);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR>), gq, dim3(256), 4 * kTile * D * 2, st, a);
+  constexpr int KS = dq_ks<D>();
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hq), dim3(256 * KS),
+                     dq_smem_bytes<D>(), st, a);
 }
 }  // namespace
 
