@@ -132,6 +132,28 @@ struct TileLoader {
   }
 };
 
+// 64-row tile filled by LDS-DMA (global_load_lds_dwordx4): no staging registers.  The LDS image
+// is lane-linear per wave-instruction (1 KiB = 64 chunks), so the XOR swizzle goes on the SOURCE
+// address: LDS chunk position `pos` of row `row` receives global chunk pos ^ swz(row), which is
+// exactly the image toff() addresses.  Completion: the __syncthreads() that ends the iteration
+// waits vmcnt(0) before anyone reads the buffer.
+template <int D>
+struct GldsTile {
+  static constexpr int CH = D / 8;
+  static constexpr int NI = kTile * CH / 256;   // wave-instructions per wave (4 waves per tile)
+  DLTB_DEV static void load(const bf16_t* base, long stride, int row0, char* tile, int wv, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int lin = (wv * NI + i) * 64 + lane;
+      const int row = lin / CH, pos = lin % CH;
+      const bf16_t* src = base + (long)(row0 + row) * stride + ((pos ^ swz<D>(row)) << 3);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(tile + (wv * NI + i) * 1024),
+                                       16, 0, 0);
+    }
+  }
+};
+
 // store a transposed 32x32-per-dt accumulator set: lane (row = lane & 31, h), reg i ->
 // column dt*32 + (i&3) + 8(i>>2) + 4h, scaled
 template <int D>
@@ -150,32 +172,29 @@ DLTB_DEV void store_acc_rows(bf16_t* dst_row, const f32x16* acc, float scale, in
 
 // =============================================================================== dropout mask
 // word (bh, t, h, q) at ((bh*nT + t)*2 + h)*T + q; bit 16n + i <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h
-__global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ mask, long BH, int T,
-                                                        uint32_t thr16, const int64_t* __restrict__ seed_ptr,
-                                                        int64_t site) {
+__global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ mask, int T, uint32_t thr16,
+                                                        const int64_t* __restrict__ seed_ptr, int64_t site) {
+  // grid: x = query chunks of 256, y = (bh * nT + t) * 2 + h  (32-bit index math only)
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= T) return;
   const int nT = T / kTile;
-  const long total = BH * nT * 2 * T;
+  const uint32_t g = blockIdx.y;
+  const int h = g & 1;
+  const int t = (g >> 1) % nT;
+  const uint32_t bh = (g >> 1) / nT;
   const uint64_t seed = site_seed(seed_ptr, site);
-  for (long wi = blockIdx.x * 256L + threadIdx.x; wi < total; wi += (long)gridDim.x * 256) {
-    const int q = (int)(wi % T);
-    long rest = wi / T;
-    const int h = (int)(rest & 1);
-    rest >>= 1;
-    const int t = (int)(rest % nT);
-    const long bh = rest / nT;
-    const uint32_t rk = rng_row_key(seed, (uint32_t)(bh * T + q));
-    uint32_t bits = 0;
+  const uint32_t rk = rng_row_key(seed, bh * (uint32_t)T + q);
+  uint32_t bits = 0;
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+  for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const uint32_t key = (uint32_t)(t * kTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
-        const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
-        bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << (16 * n + i);
-        bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << (16 * n + i + 1);
-      }
-    mask[wi] = bits;
-  }
+    for (int i = 0; i < 16; i += 2) {
+      const uint32_t key = (uint32_t)(t * kTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
+      const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
+      bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << (16 * n + i);
+      bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << (16 * n + i + 1);
+    }
+  mask[(size_t)g * T + q] = bits;
 }
 
 // =============================================================================== forward
@@ -261,12 +280,10 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   const uint32_t* mrow = DROP ? P.mask + ((long)bh * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
 
-  TileLoader<D> lk, lv;
+  const int wv = __builtin_amdgcn_readfirstlane(qw);
   if (sp < nt) {
-    lk.load(kbase, P.k_stride, sp * kTile, stid);
-    lv.load(vbase, P.v_stride, sp * kTile, stid);
-    lk.store(smem + sp * 2 * TB, stid);
-    lv.store(smem + sp * 2 * TB + TB, stid);
+    GldsTile<D>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
+    GldsTile<D>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
   }
   uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
   __syncthreads();
@@ -283,8 +300,9 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     const uint32_t mw = mw_next;
     const int tn = t + KS;
     if (tn < nt) {
-      lk.load(kbase, P.k_stride, tn * kTile, stid);
-      lv.load(vbase, P.v_stride, tn * kTile, stid);
+      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
+      GldsTile<D>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
+      GldsTile<D>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
       if (DROP) mw_next = mrow[(long)tn * 2 * T];
     }
     const int kv0 = t * kTile;
@@ -335,11 +353,6 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
             oacc[dt] = mfma32(tr_frag<D>(vt, 32 * n + 16 * s2, dt * 32, lane), pf, oacc[dt]);
         }
       }
-    }
-    if (tn < nt) {
-      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
-      lk.store(nk, stid);
-      lv.store(nk + TB, stid);
     }
     __syncthreads();
   }
@@ -457,6 +470,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const uint32_t jbit = 16 * (kw & 1) + ((r & 3) | (((r >> 3) & 3) << 2));
   const int msub = (kw >> 1) * 2 + hbit;
   const float inv_s = DROP ? 1.f / P.drop_scale : 1.f;
+  const float inv_scale = 1.f / P.scale;
 
   bfx8 kf[D / 16], vf[D / 16];
   {
@@ -489,9 +503,9 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     const long bq = (long)b * P.Hq + hq;
     lq.load(P.q + (long)b * T * P.q_stride + hq * D, P.q_stride, t * kTile, stid);
     ldo.load(P.dout + (long)b * T * P.do_stride + hq * D, P.do_stride, t * kTile, stid);
-    if (stid < kTile) {
-      vl = P.lse[bq * T + t * kTile + stid] * kLog2e;
-      vd = P.delta[bq * T + t * kTile + stid] * inv_s;
+    if (stid < kTile) {   // row constants, loaded straight into the S / dP accumulators
+      vl = -P.lse[bq * T + t * kTile + stid] * inv_scale;
+      vd = -P.delta[bq * T + t * kTile + stid] * inv_s;
     }
     if (DROP) {
       const int row = stid >> 2, sb = stid & 3;
@@ -524,50 +538,82 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     const float* dlt = lse2 + kTile;
     const uint32_t* mws = reinterpret_cast<const uint32_t*>(dlt + kTile);
     if (j + 1 < njobs) load(j + 1);
-    if (t < nT) {
+    // S' = Q K^T - lse/scale and dP' = dO V^T - delta/s: p = exp2(c S'), ds = p dP' (no dropout)
+    auto sdp = [&](int mm, f32x16& sa, f32x16& dp) {
 #pragma unroll
-      for (int mm = 0; mm < 2; ++mm) {
-        const int qb = t * kTile + 32 * mm;
-        if (CAUSAL && qb + 31 < k0) continue;   // every query < every key of this wave
-        f32x16 sa = f32x16{}, dp = f32x16{};
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          sa = mfma32(row_frag<D>(qt, 32 * mm + r, 2 * s + h), kf[s], sa);
-          dp = mfma32(row_frag<D>(dt_, 32 * mm + r, 2 * s + h), vf[s], dp);
-        }
-        const bool diag = CAUSAL && qb < k0 + 31;
-        f32x16 pd, ds;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int ql = 32 * mm + 8 * g4 + 4 * h;   // rows ql .. ql+3 for regs 4*g4 .. 4*g4+3
-          const float4 L = *reinterpret_cast<const float4*>(lse2 + ql);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int ql = 32 * mm + 8 * g4 + 4 * h;
+        const float4 L = *reinterpret_cast<const float4*>(lse2 + ql);
+        sa[4 * g4 + 0] = L.x; sa[4 * g4 + 1] = L.y; sa[4 * g4 + 2] = L.z; sa[4 * g4 + 3] = L.w;
+        if (DROP) {
+          dp[4 * g4 + 0] = 0.f; dp[4 * g4 + 1] = 0.f; dp[4 * g4 + 2] = 0.f; dp[4 * g4 + 3] = 0.f;
+        } else {
           const float4 Dl = *reinterpret_cast<const float4*>(dlt + ql);
-          const float Lv[4] = {L.x, L.y, L.z, L.w};
-          const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
+          dp[4 * g4 + 0] = Dl.x; dp[4 * g4 + 1] = Dl.y; dp[4 * g4 + 2] = Dl.z; dp[4 * g4 + 3] = Dl.w;
+        }
+      }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i = 4 * g4 + e;
-            float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -Lv[e]));
-            if (diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
-            if (DROP) {
-              const uint32_t km = keep_mask_v(mws[(ql + e) * 4 + msub], jbit);
-              pd[i] = __uint_as_float(__float_as_uint(p) & km);
-              ds[i] = p * (__uint_as_float(__float_as_uint(dp[i]) & km) - Dv[e]);
-            } else {
-              pd[i] = p;
-              ds[i] = p * (dp[i] - Dv[e]);
-            }
+      for (int s = 0; s < D / 16; ++s) {
+        sa = mfma32(row_frag<D>(qt, 32 * mm + r, 2 * s + h), kf[s], sa);
+        dp = mfma32(row_frag<D>(dt_, 32 * mm + r, 2 * s + h), vf[s], dp);
+      }
+    };
+    auto softmax = [&](int mm, const f32x16& sa, const f32x16& dp, bool diag, f32x16& pd, f32x16& ds) {
+      const int qb = t * kTile + 32 * mm;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int ql = 32 * mm + 8 * g4 + 4 * h;
+        float4 Dl;
+        if (DROP) Dl = *reinterpret_cast<const float4*>(dlt + ql);
+        const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float p = __builtin_amdgcn_exp2f(sa[i] * c);
+          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
+          if (DROP) {
+            const uint32_t km = keep_mask_v(mws[(ql + e) * 4 + msub], jbit);
+            pd[i] = __uint_as_float(__float_as_uint(p) & km);
+            ds[i] = p * (__uint_as_float(__float_as_uint(dp[i]) & km) + Dv[e]);
+          } else {
+            pd[i] = p;
+            ds[i] = p * dp[i];
           }
         }
+      }
+    };
+    auto accum = [&](int mm, const f32x16& pd, const f32x16& ds) {
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bfx8 pf = pack_frag<D>(pd, s2);
-          const bfx8 sf = pack_frag<D>(ds, s2);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bfx8 pf = pack_frag<D>(pd, s2);
+        const bfx8 sf = pack_frag<D>(ds, s2);
 #pragma unroll
-          for (int d_ = 0; d_ < NACC; ++d_) {
-            dv[d_] = mfma32(tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane), pf, dv[d_]);
-            dk[d_] = mfma32(tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane), sf, dk[d_]);
-          }
+        for (int d_ = 0; d_ < NACC; ++d_) {
+          dv[d_] = mfma32(tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane), pf, dv[d_]);
+          dk[d_] = mfma32(tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane), sf, dk[d_]);
+        }
+      }
+    };
+    if (t < nT) {
+      if (!CAUSAL || t * kTile >= k0 + 31) {
+        // full tile (no mask): both sub-tiles' S/dP first, so the second pair's MFMAs overlap the
+        // first sub-tile's softmax, and its dV/dK MFMAs overlap the second softmax
+        f32x16 sa0, dp0, sa1, dp1, pd, ds;
+        sdp(0, sa0, dp0);
+        sdp(1, sa1, dp1);
+        softmax(0, sa0, dp0, false, pd, ds);
+        accum(0, pd, ds);
+        softmax(1, sa1, dp1, false, pd, ds);
+        accum(1, pd, ds);
+      } else {
+#pragma unroll
+        for (int mm = 0; mm < 2; ++mm) {
+          const int qb = t * kTile + 32 * mm;
+          if (qb + 31 < k0) continue;   // every query < every key of this wave
+          f32x16 sa, dp, pd, ds;
+          sdp(mm, sa, dp);
+          softmax(mm, sa, dp, qb < k0 + 31, pd, ds);
+          accum(mm, pd, ds);
         }
       }
     }
@@ -635,21 +681,20 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
       of[s] = __builtin_bit_cast(bfx8, ld16<uint4>(dorow + 16 * s + 8 * h));
     }
   }
-  const float lse2 = P.lse[bq * T + qi] * kLog2e;
-  const float dl = P.delta[bq * T + qi] * (DROP ? 1.f / P.drop_scale : 1.f);
+  const float nl = -P.lse[bq * T + qi] / P.scale;                                  // S' = S - lse/scale
+  const float nd = -P.delta[bq * T + qi] * (DROP ? 1.f / P.drop_scale : 1.f);     // dP' = dP - delta/s
   const uint32_t* mrow = DROP ? P.mask + ((long)bq * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
+  const float nlc = nl * c;
   const int nt = CAUSAL ? min(nT, (qb * kBlockRows + kBlockRows - 1) / kTile + 1) : nT;
   const int nit = (nt + KS - 1) / KS;
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
 
-  TileLoader<D> lk, lv;
+  const int wv = __builtin_amdgcn_readfirstlane(qw);
   if (sp < nt) {
-    lk.load(kbase, P.k_stride, sp * kTile, stid);
-    lv.load(vbase, P.v_stride, sp * kTile, stid);
-    lk.store(smem + sp * 2 * TB, stid);
-    lv.store(smem + sp * 2 * TB + TB, stid);
+    GldsTile<D>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
+    GldsTile<D>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
   }
   uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
   __syncthreads();
@@ -665,8 +710,9 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
     const uint32_t mw = mw_next;
     const int tn = t + KS;
     if (tn < nt) {
-      lk.load(kbase, P.k_stride, tn * kTile, stid);
-      lv.load(vbase, P.v_stride, tn * kTile, stid);
+      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
+      GldsTile<D>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
+      GldsTile<D>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
       if (DROP) mw_next = mrow[(long)tn * 2 * T];
     }
     const int kv0 = t * kTile;
@@ -684,10 +730,10 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
         f32x16 ds;
         static_for<16>([&](auto I) {
           constexpr int i = I;
-          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, -lse2));
+          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, nlc));
           if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
           const float dpv = DROP ? (n == 0 ? keep_and<I>(dp[i], mw) : keep_and<16 + I>(dp[i], mw)) : dp[i];
-          ds[i] = p * (dpv - dl);
+          ds[i] = p * (dpv + nd);
         });
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -697,11 +743,6 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
             dq[dt] = mfma32(tr_frag<D>(kt, 32 * n + 16 * s2, dt * 32, lane), sf, dq[dt]);
         }
       }
-    }
-    if (tn < nt) {
-      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
-      lk.store(nk, stid);
-      lv.store(nk + TB, stid);
     }
     __syncthreads();
   }
@@ -802,10 +843,8 @@ void dltb_attn_init_attributes() {
 
 void dltb_attn_mask(uint32_t* mask, int B, int T, int Hq, uint32_t thr16, const int64_t* seed,
                     int64_t site, hipStream_t st) {
-  const long words = dltb_attn_mask_words(B, Hq, T);
-  long g = (words + 255) / 256;
-  if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(attn_mask_kernel, dim3(g), dim3(256), 0, st, mask, (long)B * Hq, T, thr16, seed, site);
+  const dim3 grid(cdiv(T, 256), (unsigned)(B * Hq * (T / kTile) * 2));
+  hipLaunchKernelGGL(attn_mask_kernel, grid, dim3(256), 0, st, mask, T, thr16, seed, site);
 }
 
 void dltb_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse,
