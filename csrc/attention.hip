@@ -552,10 +552,16 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
           dp[4 * g4 + 0] = Dl.x; dp[4 * g4 + 1] = Dl.y; dp[4 * g4 + 2] = Dl.z; dp[4 * g4 + 3] = Dl.w;
         }
       }
+      bfx8 qa[D / 16], da[D / 16];     // all fragments first: one lgkmcnt wait, not one per MFMA
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
-        sa = mfma32(row_frag<D>(qt, 32 * mm + r, 2 * s + h), kf[s], sa);
-        dp = mfma32(row_frag<D>(dt_, 32 * mm + r, 2 * s + h), vf[s], dp);
+        qa[s] = row_frag<D>(qt, 32 * mm + r, 2 * s + h);
+        da[s] = row_frag<D>(dt_, 32 * mm + r, 2 * s + h);
+      }
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sa = mfma32(qa[s], kf[s], sa);
+        dp = mfma32(da[s], vf[s], dp);
       }
     };
     auto softmax = [&](int mm, const f32x16& sa, const f32x16& dp, bool diag, f32x16& pd, f32x16& ds) {
@@ -585,12 +591,18 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     auto accum = [&](int mm, const f32x16& pd, const f32x16& ds) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
+        bfx8 ta[NACC], tq[NACC];
+#pragma unroll
+        for (int d_ = 0; d_ < NACC; ++d_) {
+          ta[d_] = tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane);
+          tq[d_] = tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane);
+        }
         const bfx8 pf = pack_frag<D>(pd, s2);
         const bfx8 sf = pack_frag<D>(ds, s2);
 #pragma unroll
         for (int d_ = 0; d_ < NACC; ++d_) {
-          dv[d_] = mfma32(tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane), pf, dv[d_]);
-          dk[d_] = mfma32(tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane), sf, dk[d_]);
+          dv[d_] = mfma32(ta[d_], pf, dv[d_]);
+          dk[d_] = mfma32(tq[d_], sf, dk[d_]);
         }
       }
     };

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""hipBLASLt GEMM microbenchmark on the exact GEMMs of one TinyGPT / Mistral training step.
+
+    python scripts/bench_gemm.py [--model A|M7B] [--iters 30]
+
+Each linear layer contributes forward (x W^T), dgrad (dY W) and wgrad (dY^T x) products in the
+layouts the fused Functions issue them.  Prints time, TFLOP/s and the share of the step's GEMM time.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+
+def shapes(model):
+    if model == "A":
+        M, d, f, V, L = 2048, 1024, 4096, 32000, 16
+        lin = [("qkv", 3 * d, d), ("out", d, d), ("fc1", f, d), ("fc2", d, f)]
+        return M, [(n, N, K, L) for n, N, K in lin] + [("lm_head", V, d, 1)]
+    M, d, f, V, L, kvd = 4096, 4096, 14336, 32000, 32, 1024
+    lin = [("qkv", d + 2 * kvd, d), ("o", d, d), ("gate_up", 2 * f, d), ("down", d, f)]
+    return M, [(n, N, K, L) for n, N, K in lin] + [("lm_head", V, d, 1)]
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="A")
+    ap.add_argument("--iters", type=int, default=30)
+    a = ap.parse_args()
+    M, lst = shapes(a.model)
+    dt = torch.bfloat16
+    rows, total = [], 0.0
+    for name, N, K, reps in lst:
+        x = torch.randn(M, K, device="cuda", dtype=dt)
+        w = torch.randn(N, K, device="cuda", dtype=dt)
+        dy = torch.randn(M, N, device="cuda", dtype=dt)
+        y = torch.empty(M, N, device="cuda", dtype=dt)
+        dx = torch.empty(M, K, device="cuda", dtype=dt)
+        dw = torch.empty(N, K, device="cuda", dtype=dt)
+        fl = 2.0 * M * N * K
+        for kind, fn in (("fwd", lambda: torch.mm(x, w.t(), out=y)),
+                         ("dgrad", lambda: torch.mm(dy, w, out=dx)),
+                         ("wgrad", lambda: torch.mm(dy.t(), x, out=dw))):
+            us = timeit(fn, a.iters)
+            total += us * reps
+            rows.append((name, kind, M, N, K, reps, us, fl / us / 1e6))
+    for name, kind, m, n, k, reps, us, tf in rows:
+        print(f"{name:8s} {kind:6s} M{m:6d} N{n:6d} K{k:6d} x{reps:3d} {us:8.1f} us {tf:7.1f} TF/s "
+              f"{100 * us * reps / total:5.1f}%")
+    print(f"total GEMM time per step (1 micro-batch): {total / 1e3:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
