@@ -475,6 +475,92 @@ void norm_bwd_dgamma(const Tensor& dy, const Tensor& s, const optional<Tensor>& 
                        cur_stream());
 }
 
+// ------------------------------------------------------------------ batched column reductions
+// colpart: one launch computing fp32 column partials of up to 3 segments (see colreduce.hip).
+// Returns the partial tensors ([nout, P, k] f32; nout = 2 for LayerNorm segments).
+std::vector<Tensor> colpart(const std::vector<int64_t>& kinds, const std::vector<Tensor>& a,
+                            const std::vector<optional<Tensor>>& b,
+                            const std::vector<optional<Tensor>>& dst,
+                            const std::vector<optional<Tensor>>& mean,
+                            const std::vector<optional<Tensor>>& rstd, double p,
+                            const optional<Tensor>& seed, const std::vector<int64_t>& sites) {
+  const size_t n = kinds.size();
+  TORCH_CHECK(n >= 1 && n <= 3, "colpart: 1..3 segments");
+  TORCH_CHECK(a.size() == n && b.size() == n && dst.size() == n && mean.size() == n && rstd.size() == n &&
+              sites.size() == n, "colpart: list lengths");
+  int64_t N0 = -1;
+  std::vector<Tensor> parts;
+  DltbColPartSeg segs[3];
+  const int64_t* sp = nullptr;
+  for (size_t i = 0; i < n; ++i) {
+    const int kind = (int)kinds[i];
+    check_contig_bf16(a[i], "colpart a");
+    check_align16(a[i], "colpart a");
+    const int64_t k = a[i].size(-1);
+    const int64_t N = a[i].numel() / k;
+    TORCH_CHECK(k % 8 == 0, "colpart: k % 8");
+    if (N0 < 0) N0 = N;
+    TORCH_CHECK(N == N0, "colpart: segments must share the row count");
+    DltbColPartSeg& S = segs[i];
+    S = DltbColPartSeg{};
+    S.a = reinterpret_cast<const uint16_t*>(a[i].data_ptr());
+    S.N = (int)N;
+    S.k = (int)k;
+    S.kind = kind;
+    S.site = sites[i];
+    if (kind == DLTB_COLPART_GELU || kind == DLTB_COLPART_LN || kind == DLTB_COLPART_RMS) {
+      TORCH_CHECK(b[i].has_value(), "colpart: second input");
+      check_contig_bf16(*b[i], "colpart b");
+      TORCH_CHECK(b[i]->sizes() == a[i].sizes(), "colpart: b shape");
+      S.b = reinterpret_cast<const uint16_t*>(b[i]->data_ptr());
+    }
+    if (kind == DLTB_COLPART_GELU || kind == DLTB_COLPART_DROP) {
+      TORCH_CHECK(dst[i].has_value(), "colpart: dst");
+      check_contig_bf16(*dst[i], "colpart dst");
+      TORCH_CHECK(dst[i]->sizes() == a[i].sizes(), "colpart: dst shape");
+      S.dst = reinterpret_cast<uint16_t*>(dst[i]->data_ptr());
+    }
+    if (kind == DLTB_COLPART_LN || kind == DLTB_COLPART_RMS) {
+      TORCH_CHECK(rstd[i].has_value() && rstd[i]->numel() == N && rstd[i]->scalar_type() == at::kFloat,
+                  "colpart: rstd");
+      S.rstd = rstd[i]->data_ptr<float>();
+      if (kind == DLTB_COLPART_LN) {
+        TORCH_CHECK(mean[i].has_value() && mean[i]->numel() == N && mean[i]->scalar_type() == at::kFloat,
+                    "colpart: mean");
+        S.mean = mean[i]->data_ptr<float>();
+      }
+    }
+    if (kind == DLTB_COLPART_DROP) sp = seed_ptr(seed, p);
+    const int P = dltb_colpart_partials((int)N);
+    Tensor part = at::empty({kind == DLTB_COLPART_LN ? 2 : 1, P, k}, a[i].options().dtype(at::kFloat));
+    S.part = part.data_ptr<float>();
+    parts.push_back(part);
+  }
+  dltb_colpart(segs, (int)n, dltb_colpart_partials((int)N0), thr_of(p), scale_of(p), sp, cur_stream());
+  return parts;
+}
+
+// colreduce_multi: parts[i] ([P, k] f32, contiguous) summed into outs[i] (bf16, k elements)
+void colreduce_multi(const std::vector<Tensor>& parts, const std::vector<Tensor>& outs,
+                     const std::vector<bool>& accumulate) {
+  const size_t n = parts.size();
+  TORCH_CHECK(n >= 1 && n <= DLTB_COLRED_MAX && outs.size() == n && accumulate.size() == n,
+              "colreduce_multi: 1..", DLTB_COLRED_MAX, " segments");
+  DltbColRedSeg segs[DLTB_COLRED_MAX];
+  for (size_t i = 0; i < n; ++i) {
+    check_cuda(parts[i], "part");
+    TORCH_CHECK(parts[i].scalar_type() == at::kFloat && parts[i].is_contiguous() && parts[i].dim() == 2,
+                "colreduce_multi: part must be contiguous f32 [P, k]");
+    check_contig_bf16(outs[i], "colreduce out");
+    const int64_t k = parts[i].size(1);
+    TORCH_CHECK(outs[i].numel() == k && k % 4 == 0, "colreduce_multi: out size / k % 4");
+    check_align16(parts[i], "part");
+    segs[i] = DltbColRedSeg{parts[i].data_ptr<float>(), reinterpret_cast<uint16_t*>(outs[i].data_ptr()),
+                            (int)parts[i].size(0), (int)k, accumulate[i] ? 1 : 0};
+  }
+  dltb_colreduce_multi(segs, (int)n, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -503,5 +589,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
+  m.def("colpart", &colpart);
+  m.def("colreduce_multi", &colreduce_multi);
   m.def("arch", []() { return std::string("gfx950"); });
 }

@@ -79,3 +79,27 @@ void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, c
                         int B, int T, int Hq, int Hkv, int D, float scale, int causal,
                         uint32_t thr16, float drop_scale, hipStream_t st);
 void dltb_attn_init_attributes();
+
+// ---- batched column reductions (colreduce.hip)
+enum { DLTB_COLPART_PLAIN = 0, DLTB_COLPART_GELU = 1, DLTB_COLPART_DROP = 2, DLTB_COLPART_LN = 3,
+       DLTB_COLPART_RMS = 4 };
+#define DLTB_COLRED_MAX 12
+struct DltbColPartSeg {
+  const uint16_t* a;
+  const uint16_t* b;
+  uint16_t* dst;
+  const float* mean;
+  const float* rstd;
+  float* part;
+  int N, k, kind;
+  int64_t site;
+};
+struct DltbColRedSeg {
+  const float* part;
+  uint16_t* out;
+  int P, k, accumulate;
+};
+int dltb_colpart_partials(int N);
+void dltb_colpart(const DltbColPartSeg* segs, int nseg, int P, uint32_t thr16, float drop_scale,
+                  const int64_t* seed, hipStream_t st);
+void dltb_colreduce_multi(const DltbColRedSeg* segs, int nseg, hipStream_t st);

@@ -134,7 +134,8 @@ class _LayerFn(torch.autograd.Function):
         dgu = F_.swiglu_bwd(dhh, gu)
         F_.linear_wgrad(dgu, h2, s[4][0], None, s[4][1])
         dh2 = torch.mm(dgu, wgu)
-        dx1 = F_.norm_bwd(dh2, x1, w_post, None, rstd2, dx2, s[3][0], None, s[3][1], True)
+        red = F_.GradReducer()
+        dx1 = F_.norm_bwd(dh2, x1, w_post, None, rstd2, dx2, s[3][0], None, s[3][1], True, red=red)
         F_.linear_wgrad(dx1, o, s[2][0], None, s[2][1])
         do = torch.mm(dx1, wo)
         qd, kd = Hq * D, Hkv * D
@@ -145,7 +146,8 @@ class _LayerFn(torch.autograd.Function):
         F_.rope_(dqkv, cos, sin, T, Hq + Hkv, D, True)      # RoPE is orthogonal: grad = R(-theta) g
         F_.linear_wgrad(dqkv, h1, s[1][0], None, s[1][1])
         dh1 = torch.mm(dqkv, wqkv)
-        dx = F_.norm_bwd(dh1, x, w_in, None, rstd1, dx1, s[0][0], None, s[0][1], True)
+        dx = F_.norm_bwd(dh1, x, w_in, None, rstd1, dx1, s[0][0], None, s[0][1], True, red=red)
+        red.flush()
         rt.grads_ready(unit)
         rt.release_backward(unit)
         return dx, None, None

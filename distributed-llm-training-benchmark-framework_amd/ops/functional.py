@@ -27,8 +27,61 @@ def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0):
     return ref.norm_fwd(x, r, w, b, eps, rms, p, seed, site)
 
 
-def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None):
-    """dx on the current stream; dgamma/dbeta (parameter gradients) on ``par``'s side stream."""
+# colpart segment kinds (csrc/colreduce.hip)
+_PLAIN, _GELU, _DROP, _LN, _RMS = 0, 1, 2, 3, 4
+
+
+class GradReducer:
+    """Batches the column reductions of one backward unit: producer kernels write fp32 column
+    partials (``colpart``) and register them here; :meth:`flush` sums every set into its bf16
+    gradient slot with ONE ``colreduce_multi`` launch (instead of one reduce launch per bias /
+    norm weight).  On the CPU the ops reduce immediately and this is a no-op."""
+
+    MAX = 12
+
+    def __init__(self):
+        self.parts, self.outs, self.acc = [], [], []
+
+    def add(self, part2d, out, accumulate):
+        if out is None:
+            return
+        if len(self.parts) == self.MAX:
+            self.flush()
+        self.parts.append(part2d)
+        self.outs.append(out)
+        self.acc.append(bool(accumulate))
+
+    def flush(self):
+        if self.parts:
+            ext().colreduce_multi(self.parts, self.outs, self.acc)
+            self.parts, self.outs, self.acc = [], [], []
+
+
+def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=None, bias=None):
+    """dx on the current stream; dgamma/dbeta (parameter gradients) on ``par``'s side stream.
+
+    With a :class:`GradReducer` the dgamma/dbeta partials (and, with ``bias=(src, slot, acc)``, the
+    column sum of ``src`` -- ``src="dx"`` meaning this call's output) come from ONE colpart launch
+    and are reduced at ``red.flush()``."""
+    if red is not None:
+        if _gpu(dy):
+            C = ext()
+            dx = C.norm_bwd_dx(dy, s, w, mean, rstd, dres, rms)
+            kinds, a, b, mn, rs = [_RMS if rms else _LN], [dy], [s], [mean], [rstd]
+            if bias is not None and bias[1] is not None:
+                src = dx if isinstance(bias[0], str) else bias[0]
+                kinds.append(_PLAIN), a.append(src), b.append(None), mn.append(None), rs.append(None)
+            parts = C.colpart(kinds, a, b, [None] * len(kinds), mn, rs, 0.0, None, [0] * len(kinds))
+            red.add(parts[0][0], gw, accumulate)
+            if not rms:
+                red.add(parts[0][1], gb, accumulate)
+            if len(parts) > 1:
+                red.add(parts[1][0], bias[1], bias[2])
+            return dx
+        dx = ref.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
+        if bias is not None and bias[1] is not None:
+            ref.colsum_into(dx if isinstance(bias[0], str) else bias[0], bias[1], bias[2])
+        return dx
     if _gpu(dy):
         C = ext()
         if par is None or not par.enabled:
@@ -45,8 +98,29 @@ def gelu_fwd(f):
     return ext().gelu_fwd(f) if _gpu(f) else ref.gelu_fwd(f)
 
 
-def gelu_bwd(dg, f, db, accumulate):
-    return ext().gelu_bwd(dg, f, db, accumulate) if _gpu(dg) else ref.gelu_bwd(dg, f, db, accumulate)
+def gelu_bwd(dg, f, db, accumulate, red=None):
+    """df = dg * gelu'(f); the fc1 bias gradient colsum(df) is fused (reduced at red.flush())."""
+    if _gpu(dg):
+        if red is None:
+            return ext().gelu_bwd(dg, f, db, accumulate)
+        df = torch.empty_like(dg)
+        parts = ext().colpart([_GELU], [dg], [f], [df], [None], [None], 0.0, None, [0])
+        red.add(parts[0][0], db, accumulate)
+        return df
+    return ref.gelu_bwd(dg, f, db, accumulate)
+
+
+def dropout_bwd_bias(g, p, seed, site, db, accumulate, red):
+    """dm = dropout_mask(g) / (1-p) (the Dropout backward) with colsum(dm) -> db fused."""
+    if _gpu(g):
+        dm = torch.empty_like(g)
+        parts = ext().colpart([_DROP], [g], [None], [dm], [None], [None], p, _sd(seed) if p > 0 else None, [site])
+        red.add(parts[0][0], db, accumulate)
+        return dm
+    dm = ref.dropout(None, g, p, seed, site)
+    if db is not None:
+        ref.colsum_into(dm, db, accumulate)
+    return dm
 
 
 def colsum_into(src, out, accumulate):

@@ -110,6 +110,46 @@ def test_colsum_and_dropout():
     assert abs(kept - 0.9) < 0.01
 
 
+@pytest.mark.parametrize("N", [2048, 300])
+def test_batched_column_reductions(N):
+    """colpart (PLAIN / GELU / DROP / LN / RMS segments, 3 per launch) + colreduce_multi vs torch."""
+    from dltb.ops.functional import GradReducer, _DROP, _GELU, _LN, _PLAIN, _RMS
+    C = ext()
+    d, k3 = 1024, 3072
+    dy, s_, dq, f = rnd(N, d), rnd(N, d), rnd(N, k3), rnd(N, k3)
+    dg = rnd(N, k3)
+    mean = torch.randn(N, device=DEV)
+    rstd = torch.rand(N, device=DEV) + 0.5
+    sd = seed_obj(77)
+    df, dm = torch.empty_like(dg), torch.empty_like(dy)
+    parts_a = C.colpart([_LN, _PLAIN, _GELU], [dy, dq, dg], [s_, None, f], [None, None, df],
+                        [mean, None, None], [rstd, None, None], 0.0, None, [0, 0, 0])
+    parts_b = C.colpart([_RMS, _DROP], [dy, dy], [s_, None], [None, dm], [None, None], [rstd, None], 0.1,
+                        sd.device_tensor, [0, 5])
+    outs = [torch.zeros(n, device=DEV, dtype=torch.bfloat16) for n in (d, d, k3, k3, d, d)]
+    outs[1].fill_(1.0)                                       # accumulate into a non-zero slot
+    red = GradReducer()
+    red.add(parts_a[0][0], outs[0], False)
+    red.add(parts_a[0][1], outs[1], True)
+    red.add(parts_a[1][0], outs[2], False)
+    red.add(parts_a[2][0], outs[3], False)
+    red.add(parts_b[0][0], outs[4], False)
+    red.add(parts_b[1][0], outs[5], False)
+    red.flush()
+    x32 = s_.float()
+    xh = (x32 - mean[:, None]) * rstd[:, None]
+    close(outs[0], (dy.float() * xh).sum(0), 0.5, 2e-2, "LN dgamma")
+    close(outs[1], dy.float().sum(0) + 1.0, 0.5, 2e-2, "LN dbeta (accumulate)")
+    close(outs[2], dq.float().sum(0), 0.5, 2e-2, "plain colsum")
+    rdf = ref.gelu_bwd(dg, f, None, False)
+    close(df, rdf, 2e-2, 2e-2, "gelu df")
+    close(outs[3], df.float().sum(0), 0.5, 2e-2, "gelu bias")
+    close(outs[4], (dy.float() * x32 * rstd[:, None]).sum(0), 0.5, 2e-2, "RMS dgamma")
+    rdm = ref.dropout(None, dy, 0.1, sd, 5)
+    assert torch.equal(dm, rdm), "dropout mask / scale"
+    close(outs[5], dm.float().sum(0), 0.5, 2e-2, "dropout bias")
+
+
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
