@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--accum-semantics", default="reference", choices=["reference", "uniform"])
     ap.add_argument("--no-align", action="store_true", help="do not align warmup to accumulation windows")
+    ap.add_argument("--graphs", default="on", choices=["on", "off"],
+                    help="replay each micro-step as a captured HIP graph (DLTB_GRAPHS overrides)")
     ap.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
                     help="hipBLASLt GEMM solutions from configs/tunableop (auto = use if present)")
     args = ap.parse_args()
@@ -61,6 +63,7 @@ def main():
     from dltb.harness import _engine_for
     from dltb.models import build_model, get_model_config
     from dltb.ops._ext import ext
+    from dltb.parallel import GraphedStep, graphs_enabled
     from dltb.utils.dist import all_reduce_max, barrier, cleanup_distributed, setup_distributed
     from dltb.utils.gemm_tuning import flush_tunableop, setup_tunableop
 
@@ -88,8 +91,13 @@ def main():
     if not args.no_align and accum > 1:
         warm = int(math.ceil(warm / accum) * accum)      # timed region starts at a window boundary
 
+    use_graphs = graphs_enabled(args.graphs, device)
+    runner = GraphedStep(engine) if use_graphs else None
+
     def one_step():
         b = next(batches)
+        if runner is not None:
+            return runner(b, b)
         loss = engine(b, b)[1]
         engine.backward(loss)
         engine.step()
@@ -144,6 +152,7 @@ def main():
             "baseline_note": "vs_baseline = value / 18147 tok/s (reference best: ZeRO-2 on 4x A10, BASELINE.md)",
             "same_strategy_published": BASELINES.get(args.strategy),
             "gemm_tuning": tmode,
+            "hip_graphs": use_graphs,
         }
         print(json.dumps(out), flush=True)
     flush_tunableop()

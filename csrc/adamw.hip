@@ -39,8 +39,13 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
     float* __restrict__ master, float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
     const G* __restrict__ grad, const int* __restrict__ blk_seg, const int64_t* __restrict__ blk_start,
     const int64_t* __restrict__ seg_ostart, const int64_t* __restrict__ seg_len,
-    const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, float lr, float beta1,
-    float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
+    const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, const float* __restrict__ hp,
+    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
+  if (hp) {   // step-dependent hyper-parameters from device memory (HIP-graph replays)
+    lr = hp[0];
+    step_size = hp[1];
+    inv_sqrt_bc2 = hp[2];
+  }
   const int seg = blk_seg[blockIdx.x];
   const int64_t start = blk_start[blockIdx.x];
   const int64_t seg_end = seg_ostart[seg] + seg_len[seg];
@@ -77,9 +82,13 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
   }
 }
 
+// sum of squares in a FIXED order (bitwise reproducible: eager runs, graph replays and ranks agree):
+// a grid-stride pass writes one partial per block, a one-block pass adds them in index order.
+constexpr int kSumsqBlocks = 1024;
+
 template <typename G>
 __global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ x, long n4,
-                                                   float* __restrict__ out) {
+                                                   float* __restrict__ part) {
   __shared__ float red[4];
   float acc = 0.f;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
@@ -88,7 +97,16 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ x, lon
     acc += g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) atomicAdd(out, acc);
+  if (threadIdx.x == 0) part[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void sumsq_final_kernel(const float* __restrict__ part, int n,
+                                                         float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) acc += part[i];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] += acc;
 }
 
 // norm_sq[0] (already all-reduced) -> coef = min(1, max_norm / (sqrt(norm_sq) + 1e-6)), norm
@@ -113,29 +131,32 @@ int dltb_adamw_chunk() { return kAdamChunk; }
 
 void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* grad, bool grad_bf16,
                 const int* blk_seg, const int64_t* blk_start, int nblocks, const int64_t* seg_ostart,
-                const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, float lr,
-                float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2,
-                hipStream_t st) {
+                const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, const float* hp,
+                float lr, float beta1, float beta2, float eps, float wd, float step_size,
+                float inv_sqrt_bc2, hipStream_t st) {
   if (nblocks <= 0) return;
   if (grad_bf16)
     hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
                        exp_avg, exp_avg_sq, (const bf16_t*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
   else
     hipLaunchKernelGGL(adamw_kernel<float>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
                        exp_avg, exp_avg_sq, (const float*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
 }
 
-void dltb_sumsq(const void* x, bool bf16, long n, float* out, hipStream_t st) {
+int dltb_sumsq_partials() { return kSumsqBlocks; }
+
+void dltb_sumsq(const void* x, bool bf16, long n, float* out, float* part, hipStream_t st) {
   const long n4 = n / 4;
   long g = (n4 + 255) / 256;
-  if (g > 1024) g = 1024;
+  if (g > kSumsqBlocks) g = kSumsqBlocks;
   if (g < 1) g = 1;
   if (bf16)
-    hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, n4, out);
+    hipLaunchKernelGGL(sumsq_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)x, n4, part);
   else
-    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, n4, out);
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, n4, part);
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, st, part, (int)g, out);
 }
 
 void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* norm_out,

@@ -279,7 +279,7 @@ void adamw(const Tensor& master, const Tensor& exp_avg, const Tensor& exp_avg_sq
            const Tensor& grad, const Tensor& blk_seg, const Tensor& blk_start,
            const Tensor& seg_ostart, const Tensor& seg_len, const Tensor& seg_dst,
            const optional<Tensor>& gscale, double lr, double beta1, double beta2, double eps,
-           double wd, int64_t step) {
+           double wd, int64_t step, const optional<Tensor>& hp) {
   for (auto* t : {&master, &exp_avg, &exp_avg_sq}) {
     check_cuda(*t, "adam state");
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "adam state f32 contiguous");
@@ -301,10 +301,16 @@ void adamw(const Tensor& master, const Tensor& exp_avg, const Tensor& exp_avg_sq
     TORCH_CHECK(gscale->scalar_type() == at::kFloat, "gscale f32");
     gs = gscale->data_ptr<float>();
   }
+  const float* hpp = nullptr;      // [lr, lr/bc1, 1/sqrt(bc2)] on the device: graph-replay safe
+  if (hp.has_value()) {
+    check_cuda(*hp, "hp");
+    TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->numel() >= 3, "adam hp: f32[>=3]");
+    hpp = hp->data_ptr<float>();
+  }
   dltb_adamw(master.data_ptr<float>(), exp_avg.data_ptr<float>(), exp_avg_sq.data_ptr<float>(),
              grad.data_ptr(), grad.scalar_type() == at::kBFloat16, blk_seg.data_ptr<int>(),
              blk_start.data_ptr<int64_t>(), (int)blk_seg.numel(), seg_ostart.data_ptr<int64_t>(),
-             seg_len.data_ptr<int64_t>(), seg_dst.data_ptr<int64_t>(), gs, (float)lr, (float)beta1,
+             seg_len.data_ptr<int64_t>(), seg_dst.data_ptr<int64_t>(), gs, hpp, (float)lr, (float)beta1,
              (float)beta2, (float)eps, (float)wd, (float)(lr / bc1), (float)(1.0 / std::sqrt(bc2)),
              cur_stream());
 }
@@ -315,8 +321,9 @@ void sumsq_(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.is_contiguous() && x.numel() % 4 == 0, "sumsq: contiguous, numel % 4");
   TORCH_CHECK(out.scalar_type() == at::kFloat, "sumsq out f32");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "sumsq dtype");
+  Tensor part = at::empty({dltb_sumsq_partials()}, out.options());
   dltb_sumsq(x.data_ptr(), x.scalar_type() == at::kBFloat16, x.numel(), out.data_ptr<float>(),
-             cur_stream());
+             part.data_ptr<float>(), cur_stream());
 }
 
 void clip_coef(const Tensor& norm_sq, double max_norm, const Tensor& coef,
@@ -561,6 +568,16 @@ void colreduce_multi(const std::vector<Tensor>& parts, const std::vector<Tensor>
   dltb_colreduce_multi(segs, (int)n, cur_stream());
 }
 
+// dst[C, R] = src[R, C]^T (bf16, both contiguous)
+void transpose_into(const Tensor& src, const Tensor& dst) {
+  check_contig_bf16(src, "src");
+  check_contig_bf16(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && dst.size(0) == src.size(1) && dst.size(1) == src.size(0),
+              "transpose_into: shapes");
+  TORCH_CHECK(src.size(1) % 4 == 0 && src.size(0) % 4 == 0, "transpose_into: dims % 4");
+  dltb_transpose(src.data_ptr(), dst.data_ptr(), (int)src.size(0), (int)src.size(1), cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -590,6 +607,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
   m.def("colpart", &colpart);
+  m.def("transpose_into", &transpose_into);
   m.def("colreduce_multi", &colreduce_multi);
   m.def("arch", []() { return std::string("gfx950"); });
 }

@@ -9,6 +9,7 @@
 //   swiglu_fwd/bwd      h = silu(gate) * up                               (Mistral-shape FFN)
 //   rope_fwd/bwd        rotate-half RoPE in place on the q/k columns of a fused qkv buffer
 //   f32_from_bf16       dst (+)= float(src)
+//   transpose           dst[C, R] = src[R, C]^T (64x64 LDS tiles; cached W^T for dgrad GEMMs)
 #include "common.h"
 
 namespace {
@@ -254,6 +255,38 @@ int colsum_splits(int N) {
   return s;
 }
 
+// ----------------------------------------------------------------------------- transpose
+// 64x64 tile through LDS (+1 column pad: conflict-free column reads); 256 threads, each moves
+// 16 elements; rows read and written as 8-byte (4 x bf16) vectors along the contiguous dim.
+__global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict__ src,
+                                                       bf16_t* __restrict__ dst, int R, int C) {
+  __shared__ bf16_t tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;     // 16 x 16 threads, 4 columns each
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r0 + ty + 16 * k, c = c0 + tx * 4;
+    if (r < R && c < C) {
+      const uint2 v = *reinterpret_cast<const uint2*>(src + (size_t)r * C + c);
+      tile[ty + 16 * k][tx * 4 + 0] = (bf16_t)(v.x & 0xFFFF);
+      tile[ty + 16 * k][tx * 4 + 1] = (bf16_t)(v.x >> 16);
+      tile[ty + 16 * k][tx * 4 + 2] = (bf16_t)(v.y & 0xFFFF);
+      tile[ty + 16 * k][tx * 4 + 3] = (bf16_t)(v.y >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = c0 + ty + 16 * k, r = r0 + tx * 4;          // output row c, columns r .. r+3
+    if (c < C && r < R) {
+      uint2 v;
+      v.x = (uint32_t)tile[tx * 4 + 0][ty + 16 * k] | ((uint32_t)tile[tx * 4 + 1][ty + 16 * k] << 16);
+      v.y = (uint32_t)tile[tx * 4 + 2][ty + 16 * k] | ((uint32_t)tile[tx * 4 + 3][ty + 16 * k] << 16);
+      *reinterpret_cast<uint2*>(dst + (size_t)c * R + r) = v;
+    }
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- API
@@ -326,4 +359,9 @@ void dltb_f32_from_bf16(float* dst, const void* src, long n, int accumulate, hip
   const long n8 = n / 8;
   hipLaunchKernelGGL(f32_from_bf16_kernel, dim3(ew_grid(n8)), dim3(256), 0, st, dst,
                      (const bf16_t*)src, n8, accumulate);
+}
+
+void dltb_transpose(const void* src, void* dst, int R, int C, hipStream_t st) {
+  hipLaunchKernelGGL(transpose_kernel, dim3(cdiv(C, 64), cdiv(R, 64)), dim3(256), 0, st,
+                     (const bf16_t*)src, (bf16_t*)dst, R, C);
 }

@@ -34,6 +34,7 @@ void dltb_swiglu_bwd(const void* dh, const void* gu, void* dgu, int N, int F, hi
 void dltb_rope(void* qkv, const float* cosb, const float* sinb, int N, int T, int heads, int D,
                int stride, bool inverse, hipStream_t st);
 void dltb_f32_from_bf16(float* dst, const void* src, long n, int accumulate, hipStream_t st);
+void dltb_transpose(const void* src, void* dst, int R, int C, hipStream_t st);
 
 // embedding.hip
 void dltb_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* x, int N, int T,
@@ -54,10 +55,11 @@ void dltb_xent_fwd_bwd(void* logits, const int64_t* targets, float* loss, int N,
 int dltb_adamw_chunk();
 void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* grad, bool grad_bf16,
                 const int* blk_seg, const int64_t* blk_start, int nblocks, const int64_t* seg_ostart,
-                const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, float lr,
-                float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2,
-                hipStream_t st);
-void dltb_sumsq(const void* x, bool bf16, long n, float* out, hipStream_t st);
+                const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, const float* hp,
+                float lr, float beta1, float beta2, float eps, float wd, float step_size,
+                float inv_sqrt_bc2, hipStream_t st);
+int dltb_sumsq_partials();
+void dltb_sumsq(const void* x, bool bf16, long n, float* out, float* part, hipStream_t st);
 void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* norm_out,
                     float extra_scale, hipStream_t st);
 void dltb_fill_f32(float* x, long n, float v, hipStream_t st);

@@ -130,14 +130,14 @@ class _LayerFn(torch.autograd.Function):
         dx2 = dx2.contiguous()
         s = [rt.grad_slot(unit, j) for j in range(6)]
         F_.linear_wgrad(dx2, hh, s[5][0], None, s[5][1])
-        dhh = torch.mm(dx2, wd)
+        dhh = F_.linear_dgrad(dx2, wd, rt.weight_t(unit, 5, wd))
         dgu = F_.swiglu_bwd(dhh, gu)
         F_.linear_wgrad(dgu, h2, s[4][0], None, s[4][1])
-        dh2 = torch.mm(dgu, wgu)
+        dh2 = F_.linear_dgrad(dgu, wgu, rt.weight_t(unit, 4, wgu))
         red = F_.GradReducer()
         dx1 = F_.norm_bwd(dh2, x1, w_post, None, rstd2, dx2, s[3][0], None, s[3][1], True, red=red)
         F_.linear_wgrad(dx1, o, s[2][0], None, s[2][1])
-        do = torch.mm(dx1, wo)
+        do = F_.linear_dgrad(dx1, wo, rt.weight_t(unit, 2, wo))
         qd, kd = Hq * D, Hkv * D
         dqkv = torch.empty_like(qkv)
         F_.attn_bwd(qkv[:, :qd], qkv[:, qd:qd + kd], qkv[:, qd + kd:], o, do, lse, aux,
@@ -145,7 +145,7 @@ class _LayerFn(torch.autograd.Function):
                     1.0 / math.sqrt(D), True, 0.0, rt.seed, 0)
         F_.rope_(dqkv, cos, sin, T, Hq + Hkv, D, True)      # RoPE is orthogonal: grad = R(-theta) g
         F_.linear_wgrad(dqkv, h1, s[1][0], None, s[1][1])
-        dh1 = torch.mm(dqkv, wqkv)
+        dh1 = F_.linear_dgrad(dqkv, wqkv, rt.weight_t(unit, 1, wqkv))
         dx = F_.norm_bwd(dh1, x, w_in, None, rstd1, dx1, s[0][0], None, s[0][1], True, red=red)
         red.flush()
         rt.grads_ready(unit)

@@ -135,22 +135,22 @@ class _BlockFn(torch.autograd.Function):
         # MLP
         dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red)
         F_.linear_wgrad(dm, g, s[10][0], None, s[10][1], par)
-        dg = torch.mm(dm, w2)
+        dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
         df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red)
         F_.linear_wgrad(df, h2, s[8][0], None, s[8][1], par)
-        dh2 = torch.mm(df, w1)
+        dh2 = F_.linear_dgrad(df, w1, rt.weight_t(unit, 8, w1))
         dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False, par,
                           red, bias=("dx", s[5][0], s[5][1]))
         # attention
         F_.linear_wgrad(dx1, o, s[4][0], None, s[4][1], par)
-        do = torch.mm(dx1, wo)
+        do = F_.linear_dgrad(dx1, wo, rt.weight_t(unit, 4, wo))
         dqkv = torch.empty_like(qkv)
         F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, amask,
                     dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i), par)
         par.join()                                            # dQ (side) completes dqkv
         F_.linear_wgrad(dqkv, h1, s[2][0], None, s[2][1], par)
-        dh1 = torch.mm(dqkv, win)
+        dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False, par,
                          red, bias=(dqkv, s[3][0], s[3][1]))
         red.flush()

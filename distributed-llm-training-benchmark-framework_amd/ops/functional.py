@@ -225,6 +225,13 @@ def linear_fwd(x2d, w, b=None):
     return torch.addmm(b, x2d, w.t())
 
 
+def linear_dgrad(dy2d, w, wt=None):
+    """dX = dY W; with a cached contiguous W^T the product runs as dY (W^T)^T (hipBLASLt NT form)."""
+    if wt is not None:
+        return torch.mm(dy2d, wt.t())
+    return torch.mm(dy2d, w)
+
+
 def linear_wgrad(dy2d, x2d, dw, db, accumulate, par=None):
     """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy).  With ``par`` the
     work runs on the side stream (parameter gradients are off the critical path)."""

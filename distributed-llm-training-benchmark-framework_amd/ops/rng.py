@@ -101,7 +101,12 @@ class StepSeed:
     def next(self) -> int:
         self.state = splitmix64(self.state)
         self.value = self.state
-        if self.device_tensor is not None:
-            v = self.value - (1 << 64) if self.value >= (1 << 63) else self.value
-            self.device_tensor.fill_(v)
+        if self.device_tensor is not None and not torch.cuda.is_current_stream_capturing():
+            self.upload()
         return self.value
+
+    def upload(self):
+        """Mirror the current value into the device tensor (a graph runner calls this before each
+        replay; inside a capture ``next`` only advances the host state)."""
+        v = self.value - (1 << 64) if self.value >= (1 << 63) else self.value
+        self.device_tensor.fill_(v)

@@ -28,9 +28,12 @@ class FlatAdamW:
         self.segments = list(segments)
         self.lr, self.betas, self.eps, self.weight_decay = lr, tuple(betas), eps, weight_decay
         self.step_count = 0
+        self._lr_now = float(lr)
         self._tables = None
+        self.hp = None
         if master.is_cuda:
             self._build_tables()
+            self.hp = torch.zeros(4, dtype=torch.float32, device=master.device)
 
     def _build_tables(self):
         chunk = ext().adamw_chunk()
@@ -53,15 +56,36 @@ class FlatAdamW:
                         torch.tensor(sl, dtype=torch.int64, device=dev),
                         torch.tensor(sd, dtype=torch.int64, device=dev))
 
+    # ---- step-dependent hyper-parameters live on the device ([lr, lr/bc1, 1/sqrt(bc2)]) so a
+    # captured HIP graph of the optimizer step stays valid across replays: ``prepare`` advances
+    # the host step counter and uploads the values (skipped while a graph is being captured;
+    # the graph runner calls ``upload`` before every replay).
+    def prepare(self, lr: float):
+        self.step_count += 1
+        self._lr_now = float(lr)
+        if self.master.is_cuda and not torch.cuda.is_current_stream_capturing():
+            self.upload()
+
+    def upload(self):
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        self.hp.copy_(torch.tensor([self._lr_now, self._lr_now / bc1, 1.0 / math.sqrt(bc2), 0.0]))
+
+    def launch(self, grad: torch.Tensor, gscale: torch.Tensor = None):
+        b1, b2 = self.betas
+        ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, *self._tables, gscale,
+                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp)
+
     @torch.no_grad()
     def step(self, grad: torch.Tensor, lr: float, gscale: torch.Tensor = None):
         assert grad.numel() == self.master.numel()
-        self.step_count += 1
         b1, b2 = self.betas
         if self.master.is_cuda:
-            ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, *self._tables, gscale,
-                        lr, b1, b2, self.eps, self.weight_decay, self.step_count)
+            self.prepare(lr)
+            self.launch(grad, gscale)
             return
+        self.step_count += 1
         ref.adamw_flat(self.master, self.exp_avg, self.exp_avg_sq, grad, lr, b1, b2, self.eps,
                        self.weight_decay, self.step_count, gscale)
         for ostart, length, dst in self.segments:

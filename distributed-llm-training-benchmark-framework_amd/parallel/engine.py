@@ -117,6 +117,28 @@ class Engine(ParamRuntime):
             self.opt_steps += 1
         self.micro += 1
 
+    # ------------------------------------------------------------------ HIP-graph support
+    def replay_host_step(self):
+        """The host-side effects of one micro-step (what forward/backward/step do besides GPU
+        work), for a step whose GPU work is a HIP-graph replay: new dropout seed on the device,
+        window position, and at a window boundary the scheduler LR uploaded for the optimizer."""
+        self.seed.next()
+        self._window_pos = self.micro % self.accum
+        self._is_boundary = self._window_pos == self.accum - 1
+        if self._is_boundary:
+            lr = self.sched(self.opt_steps)
+            self.last_lr = lr
+            self.opt.prepare(lr)
+            self.opt_steps += 1
+        self.micro += 1
+
+    def upload_step_state(self):
+        """After a capture (whose host effects already ran): push the current seed / optimizer
+        hyper-parameters to the device before the first replay."""
+        self.seed.upload()
+        if self._is_boundary:
+            self.opt.upload()
+
     def train(self, mode=True):
         self.model.train(mode)
         return self

@@ -1,0 +1,85 @@
+"""HIP-graph replay of whole training micro-steps.
+
+A TinyGPT-A micro-step is ~480 kernel launches (GEMMs, the HIP kernels of dltb._C, RCCL calls)
+issued from Python autograd Functions; measured on the MI355X, the host needs as long to issue
+them as the GPU needs to run them (scripts/host_bound_check.py: enqueue/wall = 0.99), so the
+Python side sets the step time.  ``GraphedStep`` captures the GPU work of each position in the
+gradient-accumulation window (first micro-step overwrites gradient slots, middle ones
+accumulate, the last also runs clipping + fused AdamW + parameter all-gather) into one
+``torch.cuda.CUDAGraph`` per position -- HIP graphs on ROCm -- and replays it:
+
+    step k:  engine.replay_host_step()        host bookkeeping + seed / LR uploads (3 tiny ops)
+             static_idx.copy_(batch)          the next synthetic batch into the captured input
+             graph[k % accum].replay()        ~480 kernels, one launch
+
+Everything inside a captured region reads step-dependent values from device memory: the dropout
+seed (``StepSeed.device_tensor``), AdamW's lr / bias corrections (``FlatAdamW.hp``), the clip
+coefficient (computed on the device).  Graphs share one memory pool and are replayed in capture
+order.  Capture happens on the first window after an eager warm-up window (hipBLASLt handles,
+TunableOp lookups, allocator pools and lazily built tables exist by then).  Collectives (RCCL
+reduce-scatter / all-gather / all-reduce on the process group's stream) are captured with the
+rest; ``DLTB_GRAPHS=0`` or ``--graphs off`` restores eager execution.
+"""
+import os
+
+import torch
+
+
+def graphs_enabled(flag: str, device) -> bool:
+    if torch.device(device).type != "cuda":
+        return False
+    env = os.environ.get("DLTB_GRAPHS")
+    if env is not None:
+        return env == "1"
+    return flag != "off"
+
+
+class GraphedStep:
+    """``step(idx, targets) -> loss`` for one micro-step; eager until ``capture_after`` micro-steps
+    have run (that window warms everything up), then capture-and-replay per window position."""
+
+    def __init__(self, engine, capture_after: int = None):
+        self.e = engine
+        self.accum = engine.accum
+        self.capture_after = self.accum if capture_after is None else capture_after
+        self.graphs = {}
+        self.pool = None
+        self.static_idx = None
+        self.static_tgt = None
+        self.n = 0
+
+    def _eager(self, idx, tgt):
+        loss = self.e(idx, tgt)[1]
+        self.e.backward(loss)
+        self.e.step()
+        return loss
+
+    def __call__(self, idx, tgt):
+        e = self.e
+        pos = e.micro % self.accum
+        self.n += 1
+        if self.n <= self.capture_after or (not self.graphs and pos != 0):
+            return self._eager(idx, tgt)            # warm-up, then start capturing at a window start
+        if pos in self.graphs:
+            g, loss = self.graphs[pos]
+            e.replay_host_step()
+            self.static_idx.copy_(idx)
+            if tgt is not idx:
+                self.static_tgt.copy_(tgt)
+            g.replay()
+            return loss
+        if self.static_idx is None:
+            self.static_idx = idx.clone()
+            self.static_tgt = self.static_idx if tgt is idx else tgt.clone()
+        self.static_idx.copy_(idx)
+        if self.static_tgt is not self.static_idx:
+            self.static_tgt.copy_(tgt)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool):
+            loss = self._eager(self.static_idx, self.static_tgt)
+        self.pool = g.pool()
+        e.upload_step_state()
+        g.replay()
+        self.graphs[pos] = (g, loss)
+        return loss

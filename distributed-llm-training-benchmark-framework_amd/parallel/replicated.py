@@ -18,6 +18,8 @@ DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
   the bf16 chunk in place, then an in-place all-gather per bucket re-replicates the parameters.
 * ZeRO-1: like ZeRO-2 but gradients accumulate unsharded and are reduce-scattered at the boundary.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -69,6 +71,8 @@ class ReplicatedEngine(Engine):
             self.rs_out = self.acc = None
         del master_full
         self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
+        self._wt_cache = {}      # (unit index, param index) -> (optimizer step, W^T contiguous)
+        self._cache_wt = bool(cfg.extra.get("cache_weight_t", os.environ.get("DLTB_CACHE_WT", "1") == "1"))
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
         self._launched = [False] * len(L.buckets)
@@ -78,6 +82,21 @@ class ReplicatedEngine(Engine):
             self.comm_bytes_per_step = int(nbytes * (ring if self.stage == 0 else ring / 2))
 
     # ------------------------------------------------------------------ runtime interface
+    def weight_t(self, unit, i, w):
+        if not self._cache_wt or w.dim() != 2 or not w.is_cuda:
+            return None
+        key = (unit.index, i)
+        hit = self._wt_cache.get(key)
+        if hit is not None and hit[0] == self.opt_steps:
+            return hit[1]
+        if hit is not None:
+            wt = hit[1]
+        else:
+            wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+        ext().transpose_into(w, wt)          # (re-)transpose after an optimizer step (LDS-tiled HIP)
+        self._wt_cache[key] = (self.opt_steps, wt)
+        return wt
+
     def acquire(self, unit):
         return [p.detach() for p in unit.params]
 

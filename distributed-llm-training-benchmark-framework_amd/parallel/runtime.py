@@ -63,6 +63,13 @@ class ParamRuntime:
         """Parameters of another unit used by a tied consumer (the head reads wte)."""
         return self.acquire(unit)
 
+    def weight_t(self, unit: Unit, i: int, w: torch.Tensor):
+        """A contiguous transpose of 2-D parameter ``i`` of ``unit`` (the value ``w`` holds now), or
+        None.  Engines whose parameters stay put for a whole accumulation window cache it, so the
+        data-gradient GEMM dY W runs in hipBLASLt's fast NT form (dY (W^T)^T) -- 20-30 % faster at
+        M = 2048 -- for the price of one transpose per optimizer step."""
+        return None
+
     # backward
     def acquire_backward(self, unit: Unit) -> List[torch.Tensor]:
         return [p.detach() for p in unit.params]

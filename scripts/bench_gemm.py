@@ -25,12 +25,19 @@ def shapes(model):
 
 
 def timeit(fn, iters):
+    """GPU time per call: ``iters`` calls captured in one HIP graph (no host launch gaps)."""
     for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    g.replay()
     e.record()
     torch.cuda.synchronize()
     return s.elapsed_time(e) / iters * 1e3
@@ -40,6 +47,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="A")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--layouts", action="store_true", help="also time the NT-form alternatives")
     a = ap.parse_args()
     M, lst = shapes(a.model)
     dt = torch.bfloat16
@@ -52,11 +60,18 @@ def main():
         dx = torch.empty(M, K, device="cuda", dtype=dt)
         dw = torch.empty(N, K, device="cuda", dtype=dt)
         fl = 2.0 * M * N * K
-        for kind, fn in (("fwd", lambda: torch.mm(x, w.t(), out=y)),
-                         ("dgrad", lambda: torch.mm(dy, w, out=dx)),
-                         ("wgrad", lambda: torch.mm(dy.t(), x, out=dw))):
+        wT = w.t().contiguous()          # [K, N]
+        dyT, xT = dy.t().contiguous(), x.t().contiguous()
+        kinds = [("fwd", lambda: torch.mm(x, w.t(), out=y)),
+                 ("dgrad", lambda: torch.mm(dy, w, out=dx)),
+                 ("wgrad", lambda: torch.mm(dy.t(), x, out=dw))]
+        if a.layouts:
+            kinds += [("dgradT", lambda: torch.mm(dy, wT.t(), out=dx)),     # W^T cached: NT form
+                      ("wgradT", lambda: torch.mm(dyT, xT.t(), out=dw))]    # activations transposed
+        for kind, fn in kinds:
             us = timeit(fn, a.iters)
-            total += us * reps
+            if kind in ("fwd", "dgrad", "wgrad"):
+                total += us * reps
             rows.append((name, kind, M, N, K, reps, us, fl / us / 1e6))
     for name, kind, m, n, k, reps, us, tf in rows:
         print(f"{name:8s} {kind:6s} M{m:6d} N{n:6d} K{k:6d} x{reps:3d} {us:8.1f} us {tf:7.1f} TF/s "

@@ -150,6 +150,27 @@ def test_batched_column_reductions(N):
     close(outs[5], dm.float().sum(0), 0.5, 2e-2, "dropout bias")
 
 
+@pytest.mark.parametrize("R,C", [(1024, 3072), (4096, 1024), (100, 36)])
+def test_transpose_into(R, C):
+    C_ = ext()
+    src = rnd(R, C)
+    dst = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    C_.transpose_into(src, dst)
+    assert torch.equal(dst, src.t())
+
+
+def test_sumsq_is_deterministic():
+    C_ = ext()
+    x = rnd(3_000_000)
+    outs = []
+    for _ in range(3):
+        o = torch.zeros(1, device=DEV)
+        C_.sumsq_(x, o)
+        outs.append(o.item())
+    assert outs[0] == outs[1] == outs[2]
+    assert abs(outs[0] - x.float().pow(2).sum().item()) < 1e-3 * outs[0]
+
+
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
@@ -274,7 +295,7 @@ def test_adamw_matches_torch(gdtype):
         g = torch.randn(n, device=DEV).to(gdtype)
         tp.grad = g.float()
         opt.step()
-        C.adamw(master, m, v, g, *tabs, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+        C.adamw(master, m, v, g, *tabs, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, None)
     close(master, tp.detach(), 1e-6, 1e-5, "adamw master")
     close(out_bf16, tp.detach().to(torch.bfloat16), 1e-2, 1e-2, "adamw bf16 copy")
 
