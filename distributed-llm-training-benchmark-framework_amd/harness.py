@@ -26,6 +26,7 @@ import torch
 
 from .data import SyntheticDataset, make_batcher
 from .models import build_model, get_model_config
+from .parallel.graphs import GraphedStep, graphs_enabled
 from .ops._ext import available as ext_available, so_path
 from .parallel import STRATEGIES, engine_config, make_engine
 from .parallel.strategy import default_config_path, load_deepspeed_config, load_fsdp_config
@@ -75,6 +76,8 @@ def build_parser():
     p.add_argument("--timeout-min", type=int, default=30, help="collective timeout")
     p.add_argument("--log-every", type=int, default=10)
     p.add_argument("--no-extended", action="store_true", help="do not write the extended sidecar")
+    p.add_argument("--graphs", default="on", choices=["on", "off"],
+                   help="replay micro-steps as captured HIP graphs (parallel/graphs.py; off with --profile)")
     p.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
                    help="hipBLASLt GEMM solutions (TunableOp results shipped in configs/tunableop)")
     return p
@@ -135,6 +138,7 @@ def train(args):
             print(f"Starting training: {args.steps} steps, warmup={args.warmup_steps}")
             print(f"Per-device batch: {args.per_device_batch}, Grad accum: {args.grad_accum}\n", flush=True)
         engine.train()
+        runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device) and not args.profile) else None
         losses = []
         step_events = []
         host_times = []
@@ -160,9 +164,12 @@ def train(args):
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
             h0 = time.perf_counter()
-            loss = engine(batch, targets)[1]
-            engine.backward(loss)
-            engine.step()
+            if runner is not None:
+                loss = runner(batch, targets)
+            else:
+                loss = engine(batch, targets)[1]
+                engine.backward(loss)
+                engine.step()
             h1 = time.perf_counter()
             if ev1 is not None:
                 ev1.record()
@@ -204,6 +211,7 @@ def train(args):
             "tflops_per_gpu": tflops_gpu, "mfu_vs_2.5PF_dense_bf16": tflops_gpu * 1e12 / MI355X_DENSE_BF16_FLOPS,
             "train_flops_per_token": flops_tok, "params": n_params, "trainable_params": n_params,
             "model": mcfg.to_dict(), "engine": type(engine).__name__,
+            "hip_graphs": bool(runner is not None and runner.graphs and not runner.disabled),
             "engine_config": {k: (str(v) if isinstance(v, torch.dtype) else v) for k, v in vars(ecfg).items()},
             "optimizer_steps": engine.opt_steps, "last_lr": engine.last_lr,
             "grad_norm": float(engine.grad_norm.item()) if engine.grad_norm is not None else None,

@@ -47,6 +47,7 @@ class GraphedStep:
         self.static_idx = None
         self.static_tgt = None
         self.n = 0
+        self.disabled = False
 
     def _eager(self, idx, tgt):
         loss = self.e(idx, tgt)[1]
@@ -58,7 +59,7 @@ class GraphedStep:
         e = self.e
         pos = e.micro % self.accum
         self.n += 1
-        if self.n <= self.capture_after or (not self.graphs and pos != 0):
+        if self.disabled or self.n <= self.capture_after or (not self.graphs and pos != 0):
             return self._eager(idx, tgt)            # warm-up, then start capturing at a window start
         if pos in self.graphs:
             g, loss = self.graphs[pos]
@@ -75,11 +76,33 @@ class GraphedStep:
         if self.static_tgt is not self.static_idx:
             self.static_tgt.copy_(tgt)
         torch.cuda.synchronize()
+        snap = self._host_state()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
-            loss = self._eager(self.static_idx, self.static_tgt)
+        try:
+            # thread_local: the process group's watchdog thread may query events meanwhile
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
+                loss = self._eager(self.static_idx, self.static_tgt)
+        except Exception as exc:  # noqa: BLE001 - fall back to eager execution for good
+            self._restore_host_state(snap)
+            self.disabled = True
+            print(f"[dltb] HIP-graph capture failed ({type(exc).__name__}: {exc}); running eagerly", flush=True)
+            torch.cuda.synchronize()
+            return self._eager(idx, tgt)
         self.pool = g.pool()
         e.upload_step_state()
         g.replay()
         self.graphs[pos] = (g, loss)
         return loss
+
+    def _host_state(self):
+        e = self.e
+        return (e.seed.state, e.seed.value, e.micro, e.opt_steps, e.opt.step_count, dict(e._written),
+                e._window_pos, e._is_boundary, e.last_lr)
+
+    def _restore_host_state(self, s):
+        e = self.e
+        (e.seed.state, e.seed.value, e.micro, e.opt_steps, e.opt.step_count, written,
+         e._window_pos, e._is_boundary, e.last_lr) = s
+        e._written.clear()
+        e._written.update(written)
+        e.seed.upload()
