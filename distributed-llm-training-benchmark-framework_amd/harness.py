@@ -26,6 +26,7 @@ import torch
 
 from .data import SyntheticDataset, make_batcher
 from .models import build_model, get_model_config
+from .parallel.checkpoint import export_consolidated, load_checkpoint, save_checkpoint
 from .parallel.graphs import GraphedStep, graphs_enabled
 from .ops._ext import available as ext_available, so_path
 from .parallel import STRATEGIES, engine_config, make_engine
@@ -76,6 +77,9 @@ def build_parser():
     p.add_argument("--timeout-min", type=int, default=30, help="collective timeout")
     p.add_argument("--log-every", type=int, default=10)
     p.add_argument("--no-extended", action="store_true", help="do not write the extended sidecar")
+    p.add_argument("--resume", type=str, default=None, help="load a sharded checkpoint dir before training")
+    p.add_argument("--save-dir", type=str, default=None, help="write a sharded checkpoint at the end (window boundary)")
+    p.add_argument("--export-model", type=str, default=None, help="write the consolidated bf16 model (.safetensors)")
     p.add_argument("--graphs", default="on", choices=["on", "off"],
                    help="replay micro-steps as captured HIP graphs (parallel/graphs.py; off with --profile)")
     p.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
@@ -137,6 +141,10 @@ def train(args):
         if is_main:
             print(f"Starting training: {args.steps} steps, warmup={args.warmup_steps}")
             print(f"Per-device batch: {args.per_device_batch}, Grad accum: {args.grad_accum}\n", flush=True)
+        if args.resume:
+            meta = load_checkpoint(engine, args.resume)
+            if is_main:
+                print(f"Resumed from {args.resume}: optimizer step {meta['opt_steps']}", flush=True)
         engine.train()
         runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device) and not args.profile) else None
         losses = []
@@ -187,6 +195,15 @@ def train(args):
                 print(f"[Step {step:04d}] Loss: {loss.item():.4f}, Time: {h1 - h0:.3f}s", flush=True)
         barrier()
         sync()
+        if args.save_dir:
+            if engine.micro % engine.accum == 0:
+                save_checkpoint(engine, args.save_dir, {"tier": args.tier, "seq_len": args.seq_len})
+                if is_main:
+                    print(f"Checkpoint written to {args.save_dir}", flush=True)
+            elif is_main:
+                print("WARNING: --save-dir skipped: the run did not end on an accumulation boundary", flush=True)
+        if args.export_model:
+            export_consolidated(engine, args.export_model)
         timed = args.steps - args.warmup_steps
         wall = (time.perf_counter() - t_start) if (t_start is not None and timed > 0) else 0.0
         wall = all_reduce_max(wall, device)

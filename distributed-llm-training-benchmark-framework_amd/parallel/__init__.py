@@ -1,4 +1,5 @@
 """dltb.parallel — DDP, FSDP, ZeRO-2 and ZeRO-3 engines on torch.distributed (RCCL over xGMI)."""
+from .checkpoint import export_consolidated, load_checkpoint, save_checkpoint  # noqa: F401
 from .engine import Engine, EngineConfig  # noqa: F401
 from .replicated import DDPEngine, Zero2Engine  # noqa: F401
 from .graphs import GraphedStep, graphs_enabled  # noqa: F401

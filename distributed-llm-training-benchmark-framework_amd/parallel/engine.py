@@ -204,6 +204,35 @@ class Engine(ParamRuntime):
             self.grad_norm = nrm
         return self._gscale
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        """This rank's resumable state: optimizer partition (fp32 master, exp_avg, exp_avg_sq,
+        step), micro/optimizer-step counters and the dropout seed stream.  Only at a window
+        boundary (no half-accumulated gradients to carry)."""
+        if self.micro % self.accum != 0:
+            raise RuntimeError("checkpoint only at a gradient-accumulation boundary")
+        return {"format": "dltb-engine-v1", "engine": type(self).__name__, "strategy": self.cfg.strategy,
+                "world": self.world, "rank": self.rank, "accum": self.accum, "micro": self.micro,
+                "opt_steps": self.opt_steps, "seed_state": str(self.seed.state),
+                "optimizer": self.opt.state_dict()}
+
+    def load_state_dict(self, sd: dict):
+        if sd.get("format") != "dltb-engine-v1":
+            raise ValueError("not a dltb engine checkpoint")
+        for k, mine in (("engine", type(self).__name__), ("world", self.world), ("rank", self.rank)):
+            if sd[k] != mine:
+                raise ValueError(f"checkpoint {k}={sd[k]!r} does not match this run ({mine!r})")
+        if sd["optimizer"]["master"].numel() != self.opt.master.numel():
+            raise ValueError("checkpoint partition size differs (different model or layout)")
+        self.micro, self.opt_steps = int(sd["micro"]), int(sd["opt_steps"])
+        self.seed.state = int(sd["seed_state"])
+        self.seed.value = self.seed.state
+        self.opt.load_state_dict(sd["optimizer"])
+        self._after_param_load()
+
+    def _after_param_load(self):
+        """Rebuild the compute-dtype parameters from the freshly loaded master partition."""
+
     # ------------------------------------------------------------------ introspection
     def memory_report(self) -> dict:
         return {}

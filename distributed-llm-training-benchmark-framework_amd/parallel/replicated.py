@@ -175,6 +175,14 @@ class ReplicatedEngine(Engine):
                 self._works.append(dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True))
             self._wait_works()
 
+    def _after_param_load(self):
+        self._wt_cache.clear()
+        if self.stage >= 1 and self.world > 1:   # other ranks' owner parts
+            for bk in self.layout.buckets:
+                full = self.flat_param[bk.start:bk.end]
+                mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
+                dist.all_gather_into_tensor(full, mine, group=self.group)
+
     # ------------------------------------------------------------------ introspection
     def memory_report(self):
         e = self.flat_param.element_size()

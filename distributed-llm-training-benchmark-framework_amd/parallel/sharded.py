@@ -324,6 +324,14 @@ class ShardedEngine(Engine):
             mine = self.p_flat[self.rank * pc:(self.rank + 1) * pc]
             dist.all_gather_into_tensor(self.p_flat, mine, group=self.group)
 
+    def _after_param_load(self):
+        for grp in self.groups:                   # gathered copies (if any) are stale
+            self._release(grp)
+        pc = self.p_layout.owner_numel
+        if pc and self.world > 1:
+            mine = self.p_flat[self.rank * pc:(self.rank + 1) * pc]
+            dist.all_gather_into_tensor(self.p_flat, mine, group=self.group)
+
     # ------------------------------------------------------------------ introspection
     def memory_report(self):
         e = self.shard_buf.element_size()
