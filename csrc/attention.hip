@@ -29,12 +29,9 @@
 // dK/dV kernel stages 4 words per query row in LDS.  The hash runs 1x instead of 3x, and the
 // softmax kernels pay 2 VALU ops per probability for dropout.
 #include "common.h"
+#include "mfma_tiles.h"
 
 namespace {
-
-typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr int kBlockRows = 128;   // query (fwd, dq) or key (dkdv) rows per workgroup
@@ -60,45 +57,6 @@ struct AttnArgs {
   const int64_t* seed_ptr;
   int64_t site;
 };
-
-DLTB_DEV f32x16 mfma32(bfx8 a, bfx8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-template <int D>
-DLTB_DEV int swz(int row) {
-  if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
-  else return ((row & 3) << 2) | ((row >> 2) & 3);
-}
-template <int D>
-DLTB_DEV int toff(int row, int ch) {   // byte offset of 16-byte chunk `ch` of tile row `row`
-  return row * (D * 2) + ((ch ^ swz<D>(row)) << 4);
-}
-
-// A-operand row fragment: lane (r, h) <- tile[row][16s + 8h .. +7] (chunk 2s + h)
-template <int D>
-DLTB_DEV bfx8 row_frag(const char* tile, int row, int ch) {
-  uint4 v = *reinterpret_cast<const uint4*>(tile + toff<D>(row, ch));
-  return __builtin_bit_cast(bfx8, v);
-}
-
-// A-operand transposed fragment for  Y = A * X  where X is a 32x32 accumulator whose rows are
-// tile rows [row_base, row_base + 16) of k-step s.  Lane (r = lane & 31, h = lane >> 5) gets
-// element j = tile[row_base + 8(j>>2) + 4h + (j&3)][col_base + r], matching the permuted k order
-// of an accumulator used as the B operand.
-template <int D>
-DLTB_DEV bfx8 tr_frag(const char* tile, int row_base, int col_base, int lane) {
-  const int g = lane >> 4, i = lane & 15;
-  const int row = row_base + 4 * (g >> 1) + (i >> 2);
-  const int col = col_base + 16 * (g & 1) + 4 * (i & 3);
-  const char* p0 = tile + toff<D>(row, col >> 3) + (col & 7) * 2;
-  const char* p1 = tile + toff<D>(row + 8, col >> 3) + (col & 7) * 2;
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(bfx8, c);
-}
 
 // accumulator registers 8s .. 8s+7 -> bf16 B operand of k-step s
 DLTB_DEV bfx8 acc_to_frag(const f32x16& x, int s) {
@@ -128,28 +86,6 @@ struct TileLoader {
       const int cid = tid + i * 256;
       const int row = cid / CH, ch = cid % CH;
       *reinterpret_cast<uint4*>(tile + toff<D>(row, ch)) = r[i];
-    }
-  }
-};
-
-// 64-row tile filled by LDS-DMA (global_load_lds_dwordx4): no staging registers.  The LDS image
-// is lane-linear per wave-instruction (1 KiB = 64 chunks), so the XOR swizzle goes on the SOURCE
-// address: LDS chunk position `pos` of row `row` receives global chunk pos ^ swz(row), which is
-// exactly the image toff() addresses.  Completion: the __syncthreads() that ends the iteration
-// waits vmcnt(0) before anyone reads the buffer.
-template <int D>
-struct GldsTile {
-  static constexpr int CH = D / 8;
-  static constexpr int NI = kTile * CH / 256;   // wave-instructions per wave (4 waves per tile)
-  DLTB_DEV static void load(const bf16_t* base, long stride, int row0, char* tile, int wv, int lane) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int lin = (wv * NI + i) * 64 + lane;
-      const int row = lin / CH, pos = lin % CH;
-      const bf16_t* src = base + (long)(row0 + row) * stride + ((pos ^ swz<D>(row)) << 3);
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(tile + (wv * NI + i) * 1024),
-                                       16, 0, 0);
     }
   }
 };
@@ -282,8 +218,8 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
 
   const int wv = __builtin_amdgcn_readfirstlane(qw);
   if (sp < nt) {
-    GldsTile<D>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
-    GldsTile<D>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
+    GldsTile<D, kTile>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
+    GldsTile<D, kTile>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
   }
   uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
   __syncthreads();
@@ -301,8 +237,8 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     const int tn = t + KS;
     if (tn < nt) {
       char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
-      GldsTile<D>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
-      GldsTile<D>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
+      GldsTile<D, kTile>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
+      GldsTile<D, kTile>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
       if (DROP) mw_next = mrow[(long)tn * 2 * T];
     }
     const int kv0 = t * kTile;
@@ -705,8 +641,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
 
   const int wv = __builtin_amdgcn_readfirstlane(qw);
   if (sp < nt) {
-    GldsTile<D>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
-    GldsTile<D>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
+    GldsTile<D, kTile>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
+    GldsTile<D, kTile>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
   }
   uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
   __syncthreads();
@@ -723,8 +659,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
     const int tn = t + KS;
     if (tn < nt) {
       char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
-      GldsTile<D>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
-      GldsTile<D>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
+      GldsTile<D, kTile>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
+      GldsTile<D, kTile>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
       if (DROP) mw_next = mrow[(long)tn * 2 * T];
     }
     const int kv0 = t * kTile;

@@ -578,6 +578,49 @@ void transpose_into(const Tensor& src, const Tensor& dst) {
   dltb_transpose(src.data_ptr(), dst.data_ptr(), (int)src.size(0), (int)src.size(1), cur_stream());
 }
 
+// ------------------------------------------------------------------------------- GEMM
+// layout "nt": a [M, K], b [N, K] -> out [M, N];  "tn": a [K, M], b [K, N] -> out [M, N]
+// rows may be strided (views of fused buffers); the inner dimension must be contiguous.
+bool gemm_supported(int64_t M, int64_t N, int64_t K, bool tn, int64_t cfg) {
+  return dltb_gemm_supported((int)M, (int)N, (int)K, tn, (int)cfg);
+}
+
+Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const optional<Tensor>& bias,
+            bool tn, bool accumulate, int64_t splits, int64_t cfg) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm: 2-D, inner dim contiguous");
+  const int64_t M = tn ? a.size(1) : a.size(0), K = tn ? a.size(0) : a.size(1);
+  const int64_t N = tn ? b.size(1) : b.size(0);
+  TORCH_CHECK((tn ? b.size(0) : b.size(1)) == K, "gemm: K mismatch");
+  TORCH_CHECK(dltb_gemm_supported((int)M, (int)N, (int)K, tn, (int)cfg), "gemm: shape/tile not supported");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm: row strides must be 16-byte multiples");
+  check_align16(a, "a");
+  check_align16(b, "b");
+  Tensor c;
+  if (out.has_value()) {
+    c = *out;
+    check_bf16(c, "out");
+    TORCH_CHECK(c.dim() == 2 && c.size(0) == M && c.size(1) == N && c.stride(1) == 1 && c.stride(0) % 4 == 0,
+                "gemm: out shape / layout");
+  } else {
+    TORCH_CHECK(!accumulate, "gemm: accumulate needs out");
+    c = at::empty({M, N}, a.options());
+  }
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    check_contig_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm: bias size");
+    bp = bias->data_ptr();
+  }
+  Tensor part;
+  if (splits > 1) part = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
+  dltb_gemm(a.data_ptr(), b.data_ptr(), c.data_ptr(), bp, splits > 1 ? part.data_ptr<float>() : nullptr,
+            a.stride(0), b.stride(0), c.stride(0), (int)M, (int)N, (int)K, tn, accumulate ? 1 : 0,
+            (int)splits, (int)cfg, cur_stream());
+  return c;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -607,6 +650,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
   m.def("colpart", &colpart);
+  m.def("gemm", &gemm);
+  m.def("gemm_supported", &gemm_supported);
   m.def("transpose_into", &transpose_into);
   m.def("colreduce_multi", &colreduce_multi);
   m.def("arch", []() { return std::string("gfx950"); });

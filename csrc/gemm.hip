@@ -1,0 +1,253 @@
+// bf16 GEMM on MFMA for the transformer's linear layers (gfx950).
+//
+//   C[M, N] = sum_k A(m, k) B(k, n)   (+ bias[n])   (+ C  when accumulating)      fp32 accumulate
+//
+// Two operand layouts cover every product of a training step (see ops/functional.py):
+//   NT: A stored [M][K], B stored [N][K]  (both K-contiguous)  forward x W^T, dgrad dY (W^T)^T
+//   TN: A stored [K][M], B stored [K][N]  (both K-strided)     wgrad dY^T X
+// so both operands of one kernel use the same fragment read (row_frag for NT, tr_frag for TN) and
+// therefore the same k order inside an MFMA (mfma_tiles.h).
+//
+// Block = 4 waves (2 x 2), tile BM x BN x 64.  Per 64-deep k-step each wave does 4 k16 steps of
+// (BM/64) x (BN/64) v_mfma_f32_32x32x16_bf16; A and B tiles are double-buffered in LDS and filled by
+// LDS-DMA (global_load_lds_dwordx4, swizzle on the source address) one k-step ahead.  MFMA roles
+// are swapped (srcA = B fragment, srcB = A fragment) so the accumulator has m on the lane and 4
+// consecutive n per register group: the epilogue stores 8-byte bf16x4 vectors.
+// The grid walks tiles XCD-major (consecutive workgroups go to different XCDs; each XCD gets a
+// contiguous run of tiles sharing A rows in its L2).  Optional split-K writes fp32 partials
+// reduced by a second kernel (small grids: out-proj / wgrad of 1024 x 1024).
+#include "common.h"
+#include "launchers.h"
+#include "mfma_tiles.h"
+
+namespace {
+
+constexpr int kBK = 64;
+
+struct GemmArgs {
+  const bf16_t* a;
+  const bf16_t* b;
+  bf16_t* c;
+  const bf16_t* bias;
+  float* part;          // split-K partials [splits][M][N] (fp32), null without split-K
+  long lda, ldb, ldc;
+  int M, N, K;
+  int accumulate;
+  int ksplit;           // K range per split (multiple of kBK)
+};
+
+// tile image geometry: NT -> rows = m (or n), 64 k per row (D = 64 image, BM rows);
+//                      TN -> rows = k (64), BM (or BN) m per row (D = BM image, 64 rows)
+template <int BM, int BN, bool TN>
+struct Geo {
+  static constexpr int A_BYTES = BM * kBK * 2;
+  static constexpr int B_BYTES = BN * kBK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+};
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt / lgkmcnt at max)
+template <int N>
+DLTB_DEV void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int BM, int BN, bool TN, int NSTAGE>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  using G = Geo<BM, BN, TN>;
+  constexpr int WM = BM / 2, WN = BN / 2;          // wave tile
+  constexpr int FM = WM / 32, FN = WN / 32;        // 32x32 MFMA tiles per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
+  const int wm = w & 1, wn = w >> 1;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+  // ---- tile coordinates (XCD-major walk), split index
+  const int tiles_n = g.N / BN, tiles = (g.M / BM) * tiles_n;
+  const int splits = gridDim.x / tiles;
+  int L = blockIdx.x;
+  const int split = L / tiles;
+  L -= split * tiles;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  const int m0 = (idx / tiles_n) * BM, n0 = (idx % tiles_n) * BN;
+  const int kbeg = split * g.ksplit;
+  const int nk = min(g.ksplit, g.K - kbeg) / kBK;
+
+  auto load_stage = [&](int kt, int st) {
+    char* sa = smem + st * G::STAGE;
+    char* sb = sa + G::A_BYTES;
+    const int k0 = kbeg + kt * kBK;
+    if constexpr (!TN) {
+      GldsTile<64, BM, true>::load(g.a + k0, g.lda, m0, sa, wv, lane);
+      GldsTile<64, BN, true>::load(g.b + k0, g.ldb, n0, sb, wv, lane);
+    } else {
+      GldsTile<BM, kBK, true>::load(g.a + m0, g.lda, k0, sa, wv, lane);
+      GldsTile<BN, kBK, true>::load(g.b + n0, g.ldb, k0, sb, wv, lane);
+    }
+  };
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x16{};
+
+  // NSTAGE-deep LDS ring filled by LDS-DMA.  Each wave issues GLDS wave-instructions per stage;
+  // a COUNTED vmcnt (not __syncthreads' vmcnt(0)) retires only the stage about to be read, so the
+  // next NSTAGE-2 stages stay in flight across the raw s_barrier.
+  constexpr int GLDS = TN ? (GldsTile<BM, kBK>::NI + GldsTile<BN, kBK>::NI)
+                          : (GldsTile<64, BM>::NI + GldsTile<64, BN>::NI);
+#pragma unroll
+  for (int st = 0; st < NSTAGE - 1; ++st)
+    if (st < nk) load_stage(st, st);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(nk - 1 - kt, NSTAGE - 2);     // stages issued after kt that may stay in flight
+    if (ahead >= 2) wait_vm<2 * GLDS>();
+    else if (ahead == 1) wait_vm<GLDS>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();                       // every wave's part of stage kt has landed
+    if (kt + NSTAGE - 1 < nk) load_stage(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    const char* sa = smem + (kt % NSTAGE) * G::STAGE;
+    const char* sb = sa + G::A_BYTES;
+#pragma unroll
+    for (int s = 0; s < kBK / 16; ++s) {
+      bfx8 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        if constexpr (!TN) fa[i] = row_frag<64>(sa, wm * WM + 32 * i + r, 2 * s + h);
+        else fa[i] = tr_frag<BM>(sa, 16 * s, wm * WM + 32 * i, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        if constexpr (!TN) fb[j] = row_frag<64>(sb, wn * WN + 32 * j + r, 2 * s + h);
+        else fb[j] = tr_frag<BN>(sb, 16 * s, wn * WN + 32 * j, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma32(fb[j], fa[i], acc[i][j]);   // lane <-> m
+    }
+    // the NEXT iteration's barrier orders these LDS reads before stage kt's buffer is refilled
+  }
+
+  // ---- epilogue: lane -> row m, register group q -> columns n .. n+3
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * WM + 32 * i + r;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * WN + 32 * j + 8 * q + 4 * h;
+        float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        if (splits > 1) {
+          *reinterpret_cast<float4*>(g.part + ((size_t)split * g.M + m) * g.N + n) = make_float4(v[0], v[1], v[2], v[3]);
+          continue;
+        }
+        if (g.bias) {
+          const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
+          v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+        }
+        bf16_t* cp = g.c + (size_t)m * g.ldc + n;
+        if (g.accumulate) {
+          const uint2 old = *reinterpret_cast<const uint2*>(cp);
+          v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+        }
+        uint2 o;
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(cp) = o;
+      }
+    }
+  }
+}
+
+// split-K reduction: C = sum_s part[s] (+ bias) (+ C)
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int splits) {
+  const long total4 = (long)g.M * g.N / 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
+    const long e = i * 4;
+    const int m = (int)(e / g.N), n = (int)(e % g.N);
+    float4 s = *reinterpret_cast<const float4*>(g.part + e);
+    for (int k = 1; k < splits; ++k) {
+      const float4 t = *reinterpret_cast<const float4*>(g.part + (size_t)k * g.M * g.N + e);
+      s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+    }
+    float v[4] = {s.x, s.y, s.z, s.w};
+    if (g.bias) {
+      const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
+      v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+    }
+    bf16_t* cp = g.c + (size_t)m * g.ldc + n;
+    if (g.accumulate) {
+      const uint2 old = *reinterpret_cast<const uint2*>(cp);
+      v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+    }
+    uint2 o;
+    o.x = pack_bf2(v[0], v[1]);
+    o.y = pack_bf2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(cp) = o;
+  }
+}
+
+template <int BM, int BN, bool TN>
+void launch_t(const GemmArgs& g, int splits, hipStream_t st) {
+  constexpr int NSTAGE = Geo<BM, BN, TN>::STAGE <= 32768 ? 4 : 3;   // <= 128 KiB of LDS ring
+  constexpr int smem = NSTAGE * Geo<BM, BN, TN>::STAGE;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, TN, NSTAGE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, TN, NSTAGE>), dim3(tiles * splits), dim3(256), smem, st, g);
+}
+
+}  // namespace
+
+// tile config: 0 = 128x128, 1 = 256x128 (BM 256), 2 = 128x256 (BN 256)
+bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg) {
+  if (tn && cfg != 0) return false;      // TN images are 128-element rows (swizzle of mfma_tiles.h)
+  const int BM = cfg == 1 ? 256 : 128, BN = cfg == 2 ? 256 : 128;
+  return M % BM == 0 && N % BN == 0 && K % kBK == 0 && M > 0 && N > 0 && K > 0;
+}
+
+int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
+              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, hipStream_t st) {
+  GemmArgs g{};
+  g.a = (const bf16_t*)a;
+  g.b = (const bf16_t*)b;
+  g.c = (bf16_t*)c;
+  g.bias = (const bf16_t*)bias;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.accumulate = accumulate;
+  if (splits < 1) splits = 1;
+  const int kchunks = K / kBK;
+  if (splits > kchunks) splits = kchunks;
+  g.ksplit = ((kchunks + splits - 1) / splits) * kBK;
+  splits = (K + g.ksplit - 1) / g.ksplit;
+  g.part = splits > 1 ? part : nullptr;
+  if (splits > 1 && !part) return -1;
+#define DLTB_G(BM, BN)                                              \
+  do {                                                              \
+    if (tn) launch_t<BM, BN, true>(g, splits, st);                  \
+    else launch_t<BM, BN, false>(g, splits, st);                    \
+  } while (0)
+  if (cfg == 1 && !tn) launch_t<256, 128, false>(g, splits, st);
+  else if (cfg == 2 && !tn) launch_t<128, 256, false>(g, splits, st);
+  else DLTB_G(128, 128);
+#undef DLTB_G
+  if (splits > 1) {
+    long total4 = (long)M * N / 4;
+    long grid = (total4 + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(grid), dim3(256), 0, st, g, splits);
+  }
+  return splits;
+}

@@ -105,3 +105,8 @@ int dltb_colpart_partials(int N);
 void dltb_colpart(const DltbColPartSeg* segs, int nseg, int P, uint32_t thr16, float drop_scale,
                   const int64_t* seed, hipStream_t st);
 void dltb_colreduce_multi(const DltbColRedSeg* segs, int nseg, hipStream_t st);
+
+// ---- gemm.hip: C[M,N] = A B (+bias) (+C); NT: A [M][K], B [N][K]; TN: A [K][M], B [K][N]
+bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg);
+int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
+              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, hipStream_t st);

@@ -1,0 +1,98 @@
+// MFMA / LDS tile helpers shared by the attention and GEMM kernels (gfx950, CDNA4).
+//
+// * v_mfma_f32_32x32x16_bf16 wrapper: C[i][j] += sum_k A[i][k] B[k][j]; operand fragments are 8 bf16
+//   (lane l: row/col l & 31, k-half l >> 5), the accumulator holds column j = l & 31 and rows
+//   (r & 3) + 8 (r >> 2) + 4 (l >> 5) of register r.
+// * LDS tile images with rows of D bf16 (D = 64: 128-byte rows, D = 128: 256-byte rows) and a
+//   16-byte-chunk XOR swizzle that makes both read patterns bank-conflict free:
+//     row_frag - ds_read_b128 of 8 consecutive elements of one row   (K-contiguous operands)
+//     tr_frag  - 2 x ds_read_b64_tr_b16: 8 elements of one column     (K-strided operands; the k
+//                order is permuted as (j & 3) + 8 (j >> 2) + 4 h, identical for both operands)
+// * GldsTile: LDS-DMA (global_load_lds_dwordx4) fill of such an image with the swizzle applied to
+//   the SOURCE address (the LDS side of an LDS-DMA is lane-linear, 1 KiB per wave-instruction).
+#pragma once
+#include "common.h"
+
+namespace {
+
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+DLTB_DEV f32x16 mfma32(bfx8 a, bfx8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int D>
+DLTB_DEV int swz(int row) {
+  if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+  else return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+template <int D>
+DLTB_DEV int toff(int row, int ch) {   // byte offset of 16-byte chunk `ch` of tile row `row`
+  return row * (D * 2) + ((ch ^ swz<D>(row)) << 4);
+}
+
+// A-operand row fragment: lane (r, h) <- tile[row][16s + 8h .. +7] (chunk 2s + h)
+template <int D>
+DLTB_DEV bfx8 row_frag(const char* tile, int row, int ch) {
+  uint4 v = *reinterpret_cast<const uint4*>(tile + toff<D>(row, ch));
+  return __builtin_bit_cast(bfx8, v);
+}
+
+// A-operand transposed fragment for  Y = A * X  where X is a 32x32 accumulator whose rows are
+// tile rows [row_base, row_base + 16) of k-step s.  Lane (r = lane & 31, h = lane >> 5) gets
+// element j = tile[row_base + 8(j>>2) + 4h + (j&3)][col_base + r], matching the permuted k order
+// of an accumulator used as the B operand.
+template <int D>
+DLTB_DEV bfx8 tr_frag(const char* tile, int row_base, int col_base, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int row = row_base + 4 * (g >> 1) + (i >> 2);
+  const int col = col_base + 16 * (g & 1) + 4 * (i & 3);
+  const char* p0 = tile + toff<D>(row, col >> 3) + (col & 7) * 2;
+  const char* p1 = tile + toff<D>(row + 8, col >> 3) + (col & 7) * 2;
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p0);
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p1);
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bfx8, c);
+}
+
+// ROWS-row tile of D-element rows filled by LDS-DMA from a row-major global matrix (rows
+// row0 .. row0 + ROWS - 1, columns col0 .. col0 + D - 1 of `base`, row stride `stride`) by 4 waves.
+// Completion: a __syncthreads() (which waits vmcnt(0)) before anyone reads the tile.
+// One LDS-DMA instruction issued from inline asm: invisible to hipcc's waitcnt bookkeeping, so the
+// compiler does NOT insert a vmcnt(0) before the next LDS read (it would drain a multi-stage ring).
+// The caller retires it with a counted s_waitcnt vmcnt (gemm.hip wait_vm) + s_barrier.
+DLTB_DEV void glds16_asm(const void* gsrc, const void* lds_dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+
+template <int D, int ROWS, bool ASM = false>
+struct GldsTile {
+  static constexpr int CH = D / 8;
+  static constexpr int NI = ROWS * CH / 256;   // wave-instructions per wave (4 waves per tile)
+  static_assert(ROWS * CH % 256 == 0, "tile must split into whole wave-instructions");
+  DLTB_DEV static void load(const bf16_t* base, long stride, int row0, char* tile, int wv, int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int lin = (wv * NI + i) * 64 + lane;
+      const int row = lin / CH, pos = lin % CH;
+      const bf16_t* src = base + (long)(row0 + row) * stride + ((pos ^ swz<D>(row)) << 3);
+      if constexpr (ASM)
+        glds16_asm(src, tile + (wv * NI + i) * 1024);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(tile + (wv * NI + i) * 1024),
+                                         16, 0, 0);
+    }
+  }
+};
+
+}  // namespace

@@ -13,6 +13,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+import dltb  # noqa: E402,F401
+
 
 def shapes(model):
     if model == "A":
@@ -48,6 +50,7 @@ def main():
     ap.add_argument("--model", default="A")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--layouts", action="store_true", help="also time the NT-form alternatives")
+    ap.add_argument("--dltb", action="store_true", help="also time the dltb MFMA GEMM (tile configs x split-K)")
     a = ap.parse_args()
     M, lst = shapes(a.model)
     dt = torch.bfloat16
@@ -65,6 +68,17 @@ def main():
         kinds = [("fwd", lambda: torch.mm(x, w.t(), out=y)),
                  ("dgrad", lambda: torch.mm(dy, w, out=dx)),
                  ("wgrad", lambda: torch.mm(dy.t(), x, out=dw))]
+        if a.dltb:
+            from dltb.ops._ext import ext
+            C = ext()
+            for cfg in (0, 1, 2):
+                for sp in (1, 2, 4):
+                    if C.gemm_supported(M, N, K, False, cfg):
+                        kinds.append((f"fwd[c{cfg}s{sp}]", lambda cfg=cfg, sp=sp: C.gemm(x, w, y, None, False, False, sp, cfg)))
+                    if C.gemm_supported(M, K, N, False, cfg):
+                        kinds.append((f"dgT[c{cfg}s{sp}]", lambda cfg=cfg, sp=sp: C.gemm(dy, wT, dx, None, False, False, sp, cfg)))
+                    if C.gemm_supported(N, K, M, True, cfg):
+                        kinds.append((f"wg[c{cfg}s{sp}]", lambda cfg=cfg, sp=sp: C.gemm(dy, x, dw, None, True, False, sp, cfg)))
         if a.layouts:
             kinds += [("dgradT", lambda: torch.mm(dy, wT.t(), out=dx)),     # W^T cached: NT form
                       ("wgradT", lambda: torch.mm(dyT, xT.t(), out=dw))]    # activations transposed

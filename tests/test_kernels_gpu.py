@@ -171,6 +171,32 @@ def test_sumsq_is_deterministic():
     assert abs(outs[0] - x.float().pow(2).sum().item()) < 1e-3 * outs[0]
 
 
+@pytest.mark.parametrize("tn", [False, True])
+@pytest.mark.parametrize("M,N,K,cfg,splits", [(256, 384, 512, 0, 1), (512, 256, 1024, 0, 4),
+                                               (512, 256, 256, 1, 1), (256, 512, 192, 2, 2)])
+def test_gemm(tn, M, N, K, cfg, splits):
+    """dltb GEMM (NT: a[M,K] b[N,K]; TN: a[K,M] b[K,N]) vs fp32 torch, incl. bias / accumulate /
+    split-K and row-strided operand views."""
+    C_ = ext()
+    if not C_.gemm_supported(M, N, K, tn, cfg):
+        pytest.skip("tile config not offered for this layout")
+    if tn:
+        a_full, b_full = rnd(K, M + 64), rnd(K, N)
+        a, b = a_full[:, 64:], b_full                 # strided view of a wider buffer
+        ref32 = a.float().t() @ b.float()
+    else:
+        a_full, b_full = rnd(M, K + 64), rnd(N, K)
+        a, b = a_full[:, :K], b_full
+        ref32 = a.float() @ b.float().t()
+    bias = rnd(N)
+    out = C_.gemm(a, b, None, bias, tn, False, splits, cfg)
+    close(out, ref32 + bias.float(), 0.1, 2e-2, "gemm + bias")
+    prev = rnd(M, N)
+    acc = prev.clone()
+    C_.gemm(a, b, acc, None, tn, True, splits, cfg)
+    close(acc, ref32 + prev.float(), 0.1, 2e-2, "gemm accumulate")
+
+
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
