@@ -19,11 +19,7 @@
 
 namespace {
 
-DLTB_DEV float gelu_grad_c(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+DLTB_DEV float gelu_grad_c(float x) { return gelu_grad_f(x); }
 
 struct ColPartArgs {
   DltbColPartSeg seg[3];

@@ -80,6 +80,29 @@ DLTB_DEV float block_max(float v, float* red) {
   return t;
 }
 
+// ---------------------------------------------------------------- GELU (erf form, nn.GELU default)
+// erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below bf16 resolution): one v_rcp,
+// one v_exp and 6 FMAs instead of the libm erff polynomial chain -- the GELU kernels become
+// HBM-bound.  The derivative pdf term reuses the same exp(-x^2/2).
+DLTB_DEV float erf_fast(float x, float* e_out = nullptr) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+  const float e = __expf(-ax * ax);
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.f - p * t * e;
+  if (e_out) *e_out = e;
+  return copysignf(y, x);
+}
+DLTB_DEV float gelu_fwd_f(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+DLTB_DEV float gelu_grad_f(float x) {
+  float e;                                                  // e = exp(-x^2 / 2)
+  const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, &e));
+  return cdf + x * 0.39894228040143268f * e;
+}
+
 // ---------------------------------------------------------------- dropout RNG (see ops/rng.py)
 #define DLTB_C_ROW 0x9E3779B1u
 #define DLTB_C_COL 0x85EBCA77u

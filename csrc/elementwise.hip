@@ -15,12 +15,8 @@
 namespace {
 
 // ------------------------------------------------------------------------------------ GELU
-DLTB_DEV float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-DLTB_DEV float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
+DLTB_DEV float gelu_f(float x) { return gelu_fwd_f(x); }
+DLTB_DEV float gelu_grad(float x) { return gelu_grad_f(x); }
 
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict__ f,
                                                       bf16_t* __restrict__ g, long n8) {
