@@ -292,10 +292,12 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     }
     __syncthreads();
   }
-  if constexpr (KS == 2) {     // merge the two key halves: split 1 -> LDS -> split 0
+  if constexpr (KS > 1) {      // merge the key splits: splits 1..KS-1 -> LDS -> split 0
     constexpr int NF = 16 * NACC + 2;
-    float* red = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
-    if (sp == 1) {
+    static_assert((KS - 1) * 4 * NF * 64 * 4 <= 4 * KS * kTile * D * 2, "merge buffer exceeds the LDS ring");
+    float* red0 = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
+    if (sp > 0) {
+      float* red = red0 + (sp - 1) * 4 * NF * 64;
       red[0] = m;
       red[64] = l;
 #pragma unroll
@@ -304,16 +306,20 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
         for (int i = 0; i < 16; ++i) red[(2 + 16 * dt + i) * 64] = oacc[dt][i];
     }
     __syncthreads();
-    if (sp == 1) return;
-    const float m1 = red[0], l1 = red[64];
-    const float mn = fmaxf(m, m1);
-    const float a0 = __builtin_amdgcn_exp2f(m - mn), a1 = __builtin_amdgcn_exp2f(m1 - mn);
-    m = mn;
-    l = l * a0 + l1 * a1;
+    if (sp > 0) return;
 #pragma unroll
-    for (int dt = 0; dt < NACC; ++dt)
+    for (int o = 0; o < KS - 1; ++o) {
+      const float* red = red0 + o * 4 * NF * 64;
+      const float m1 = red[0], l1 = red[64];
+      const float mn = fmaxf(m, m1);
+      const float a0 = __builtin_amdgcn_exp2f(m - mn), a1 = __builtin_amdgcn_exp2f(m1 - mn);
+      m = mn;
+      l = l * a0 + l1 * a1;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] = oacc[dt][i] * a0 + red[(2 + 16 * dt + i) * 64] * a1;
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] = oacc[dt][i] * a0 + red[(2 + 16 * dt + i) * 64] * a1;
+    }
   }
   l += __shfl_xor(l, 32, 64);
   const float inv = (DROP ? P.drop_scale : 1.f) / l;
@@ -323,7 +329,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
 }
 
 template <int D>
-constexpr int fwd_ks() { return 2; }
+constexpr int fwd_ks() { return 2; }      // KS = 4 measured slower at D = 64 (VGPR spills at 128)
 template <int D>
 constexpr int fwd_smem_bytes() { return 4 * fwd_ks<D>() * kTile * D * 2; }
 

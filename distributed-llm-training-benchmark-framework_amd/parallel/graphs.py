@@ -97,12 +97,12 @@ class GraphedStep:
     def _host_state(self):
         e = self.e
         return (e.seed.state, e.seed.value, e.micro, e.opt_steps, e.opt.step_count, dict(e._written),
-                e._window_pos, e._is_boundary, e.last_lr)
+                e._window_pos, e._is_boundary, e.last_lr, e._pending_lr, e.opt._lr_now)
 
     def _restore_host_state(self, s):
         e = self.e
         (e.seed.state, e.seed.value, e.micro, e.opt_steps, e.opt.step_count, written,
-         e._window_pos, e._is_boundary, e.last_lr) = s
+         e._window_pos, e._is_boundary, e.last_lr, e._pending_lr, e.opt._lr_now) = s
         e._written.clear()
         e._written.update(written)
         e.seed.upload()

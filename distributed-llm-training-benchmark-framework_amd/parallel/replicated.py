@@ -72,6 +72,9 @@ class ReplicatedEngine(Engine):
         del master_full
         self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
         self._wt_cache = {}      # (unit index, param index) -> (optimizer step, W^T contiguous)
+        self._ag_pending = {}    # bucket -> async all-gather of updated parameters (deferred step)
+        self._defer_opt = (self.stage >= 1 and self.world > 1 and
+                           bool(cfg.extra.get("defer_opt", os.environ.get("DLTB_DEFER_OPT", "1") == "1")))
         self._cache_wt = bool(cfg.extra.get("cache_weight_t", os.environ.get("DLTB_CACHE_WT", "1") == "1"))
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
@@ -98,9 +101,17 @@ class ReplicatedEngine(Engine):
         return wt
 
     def acquire(self, unit):
+        if self._ag_pending:
+            b = self._bucket_of.get(id(unit))
+            w = self._ag_pending.pop(b, None)
+            if w is not None:
+                w.wait()
         return [p.detach() for p in unit.params]
 
     acquire_backward = acquire
+
+    def acquire_tied(self, unit):
+        return self.acquire(unit)
 
     def grad_slot(self, unit, i):
         s = self.layout.slot(unit, i)
@@ -162,12 +173,28 @@ class ReplicatedEngine(Engine):
             return self.acc
         return self.rs_out if self.world > 1 else self.flat_grad
 
-    def _optimizer_step(self, lr):
-        # (ZeRO-1 reduce-scattered its window-accumulated gradients during the boundary backward)
+    def _update(self, lr):
         g = self._owner_grad()
         extra = 1.0 / (self.world * self.accum)
         gscale = self._clip_coef([g], extra, sharded=self.stage >= 1)
         self.opt.step(g, lr, gscale)
+
+    def _deferred_optimizer_step(self, lr):
+        self._update(lr)
+        for b in reversed(range(len(self.layout.buckets))):     # forward order: embedding first
+            bk = self.layout.buckets[b]
+            full = self.flat_param[bk.start:bk.end]
+            mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
+            self._ag_pending[b] = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+
+    def _wait_param_gathers(self):
+        for w in self._ag_pending.values():
+            w.wait()
+        self._ag_pending.clear()
+
+    def _optimizer_step(self, lr):
+        # (ZeRO-1 reduce-scattered its window-accumulated gradients during the boundary backward)
+        self._update(lr)
         if self.stage >= 1 and self.world > 1:
             for bk in self.layout.buckets:
                 full = self.flat_param[bk.start:bk.end]
@@ -192,6 +219,7 @@ class ReplicatedEngine(Engine):
                 "bucket_mb": [round(b.numel * e / 2**20, 2) for b in self.layout.buckets]}
 
     def full_state_dict(self):
+        self.finalize()
         out = {}
         if self.stage >= 1 and self.world > 1:
             full = torch.zeros(self.layout.total, dtype=torch.float32, device=self.device)

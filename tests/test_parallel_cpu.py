@@ -152,3 +152,31 @@ def test_world2_matches_single_process(strategy, accum, kw):
     ref = _train(strategy, _batches(STEPS, 4), 0, 1, accum, **(dict(kw, semantics=sem) if sem != "reference" else kw))
     for n in ref:
         assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
+
+
+
+def _worker_defer(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        res = {}
+        for defer in ("1", "0"):
+            os.environ["DLTB_DEFER_OPT"] = defer
+            res[defer] = _train("zero2", _batches(STEPS, 4), rank, world, 2)
+        if rank == 0:
+            torch.save(res, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_world2_deferred_optimizer_step_is_exact():
+    """ZeRO-2 at world 2 runs the window's AdamW + parameter all-gather at the start of the next
+    micro-step (overlapping the forward); the trained weights must be bitwise identical."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "sd.pt")
+        mp.spawn(_worker_defer, args=(2, _free_port(), out), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    for n in res["1"]:
+        assert torch.equal(res["1"][n], res["0"][n]), n
