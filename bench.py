@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--accum-semantics", default="reference", choices=["reference", "uniform"])
     ap.add_argument("--no-align", action="store_true", help="do not align warmup to accumulation windows")
-    ap.add_argument("--graphs", default="on", choices=["on", "off"],
+    ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
                     help="replay each micro-step as a captured HIP graph (DLTB_GRAPHS overrides)")
     ap.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
                     help="hipBLASLt GEMM solutions from configs/tunableop (auto = use if present)")
@@ -91,7 +91,7 @@ def main():
     if not args.no_align and accum > 1:
         warm = int(math.ceil(warm / accum) * accum)      # timed region starts at a window boundary
 
-    use_graphs = graphs_enabled(args.graphs, device)
+    use_graphs = graphs_enabled(args.graphs, device, world)
     runner = GraphedStep(engine) if use_graphs else None
 
     def one_step():

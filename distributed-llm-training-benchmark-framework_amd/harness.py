@@ -80,7 +80,7 @@ def build_parser():
     p.add_argument("--resume", type=str, default=None, help="load a sharded checkpoint dir before training")
     p.add_argument("--save-dir", type=str, default=None, help="write a sharded checkpoint at the end (window boundary)")
     p.add_argument("--export-model", type=str, default=None, help="write the consolidated bf16 model (.safetensors)")
-    p.add_argument("--graphs", default="on", choices=["on", "off"],
+    p.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
                    help="replay micro-steps as captured HIP graphs (parallel/graphs.py; off with --profile)")
     p.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
                    help="hipBLASLt GEMM solutions (TunableOp results shipped in configs/tunableop)")
@@ -146,7 +146,7 @@ def train(args):
             if is_main:
                 print(f"Resumed from {args.resume}: optimizer step {meta['opt_steps']}", flush=True)
         engine.train()
-        runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device) and not args.profile) else None
+        runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device, world) and not args.profile) else None
         losses = []
         step_events = []
         host_times = []

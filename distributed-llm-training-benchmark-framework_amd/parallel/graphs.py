@@ -25,13 +25,19 @@ import os
 import torch
 
 
-def graphs_enabled(flag: str, device) -> bool:
+def graphs_enabled(flag: str, device, world: int = 1) -> bool:
+    """``on`` / ``off``, or ``auto``: on for a single process, off for multi-rank runs.  Captured
+    RCCL collectives work on this stack (scripts/rccl_graph_check.py) but a multi-rank capture
+    cannot be validated on a one-GPU box, and at 1 GPU replay gains ~1 % (the step is GPU-bound),
+    so multi-rank runs stay eager unless asked (``--graphs on`` / ``DLTB_GRAPHS=1``)."""
     if torch.device(device).type != "cuda":
         return False
     env = os.environ.get("DLTB_GRAPHS")
     if env is not None:
         return env == "1"
-    return flag != "off"
+    if flag == "auto":
+        return world == 1
+    return flag == "on"
 
 
 class GraphedStep:
