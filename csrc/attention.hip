@@ -466,7 +466,10 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
       f[stid] = vl;
       f[kTile + stid] = vd;
     }
-    if (DROP) reinterpret_cast<uint32_t*>(f + 2 * kTile)[stid] = mword;
+    if (DROP) {   // [sub][row]: a lane's 4 consecutive query rows are one ds_read_b128
+      const int row = stid >> 2, sb = stid & 3;
+      reinterpret_cast<uint32_t*>(f + 2 * kTile)[sb * kTile + row] = mword;
+    }
   };
   load(0);
   store(0);
@@ -512,15 +515,20 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
       for (int g4 = 0; g4 < 4; ++g4) {
         const int ql = 32 * mm + 8 * g4 + 4 * h;
         float4 Dl;
-        if (DROP) Dl = *reinterpret_cast<const float4*>(dlt + ql);
+        uint4 M4;
+        if (DROP) {
+          Dl = *reinterpret_cast<const float4*>(dlt + ql);
+          M4 = *reinterpret_cast<const uint4*>(mws + msub * kTile + ql);
+        }
         const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
+        const uint32_t Mv[4] = {M4.x, M4.y, M4.z, M4.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g4 + e;
           float p = __builtin_amdgcn_exp2f(sa[i] * c);
           if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
           if (DROP) {
-            const uint32_t km = keep_mask_v(mws[(ql + e) * 4 + msub], jbit);
+            const uint32_t km = keep_mask_v(Mv[e], jbit);
             pd[i] = __uint_as_float(__float_as_uint(p) & km);
             ds[i] = p * (__uint_as_float(__float_as_uint(dp[i]) & km) + Dv[e]);
           } else {
