@@ -329,7 +329,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
 }
 
 template <int D>
-constexpr int fwd_ks() { return 2; }      // KS = 4 measured slower at D = 64 (VGPR spills at 128)
+constexpr int fwd_ks() { return D == 64 ? 3 : 2; }   // KS = 4 at D = 64 spills (128 VGPRs) and is slower
 template <int D>
 constexpr int fwd_smem_bytes() { return 4 * fwd_ks<D>() * kTile * D * 2; }
 
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
 // =============================================================================== dQ
 // Query-major, KS key-splits per workgroup as in the forward; dQ partials merge through LDS.
 template <int D>
-constexpr int dq_ks() { return 2; }
+constexpr int dq_ks() { return 2; }        // KS = 3 measured neutral at D = 64 (and spills)
 template <int D>
 constexpr int dq_smem_bytes() { return 4 * dq_ks<D>() * kTile * D * 2; }
 
@@ -708,21 +708,25 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
     }
     __syncthreads();
   }
-  if constexpr (KS == 2) {
+  if constexpr (KS > 1) {      // splits 1..KS-1 -> LDS -> split 0
     constexpr int NF = 16 * NACC;
-    float* red = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
-    if (sp == 1) {
+    static_assert((KS - 1) * 4 * NF * 64 * 4 <= 4 * KS * kTile * D * 2, "merge buffer exceeds the LDS ring");
+    float* red0 = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
+    if (sp > 0) {
+      float* red = red0 + (sp - 1) * 4 * NF * 64;
 #pragma unroll
       for (int dt = 0; dt < NACC; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; ++i) red[(16 * dt + i) * 64] = dq[dt][i];
     }
     __syncthreads();
-    if (sp == 1) return;
+    if (sp > 0) return;
 #pragma unroll
-    for (int dt = 0; dt < NACC; ++dt)
+    for (int o = 0; o < KS - 1; ++o)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) dq[dt][i] += red[(16 * dt + i) * 64];
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dq[dt][i] += red0[o * 4 * NF * 64 + (16 * dt + i) * 64];
   }
   bf16_t* dqrow = P.out + ((long)b * T + qi) * P.out_stride + hq * D;
   store_acc_rows<D>(dqrow, dq, P.scale * (DROP ? P.drop_scale : 1.f), h);
