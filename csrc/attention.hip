@@ -375,8 +375,8 @@ constexpr int dkdv_stage_bytes() { return 2 * kTile * D * 2 + 2 * kTile * 4 + kT
 template <int D>
 constexpr int dkdv_smem_bytes() {
   constexpr int a = 2 * dkdv_ks<D>() * dkdv_stage_bytes<D>();
-  constexpr int merge = 4 * 64 * 4 * (2 * 16 * (D / 32));
-  return dkdv_ks<D>() == 2 && merge > a ? merge : a;
+  constexpr int merge = (dkdv_ks<D>() - 1) * 4 * 64 * 4 * (2 * 16 * (D / 32));
+  return merge > a ? merge : a;
 }
 
 DLTB_DEV float keep_and_v(float p, uint32_t mw, uint32_t bit) {
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const int nit = (nT - t_begin + KS - 1) / KS;   // iterations per head
   const int njobs = G * nit;
 
-  TileLoader<D> lq, ldo;
+  const int wv = __builtin_amdgcn_readfirstlane(kw);
   float vl = 0.f, vd = 0.f;
   uint32_t mword = 0;
   auto tile_of = [&](int j, int& g, int& t) { g = j / nit; t = t_begin + (j % nit) * KS + sp; };
@@ -443,8 +443,11 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     if (t >= nT) return;
     const int hq = hk * G + g;
     const long bq = (long)b * P.Hq + hq;
-    lq.load(P.q + (long)b * T * P.q_stride + hq * D, P.q_stride, t * kTile, stid);
-    ldo.load(P.dout + (long)b * T * P.do_stride + hq * D, P.do_stride, t * kTile, stid);
+    // Q / dO tiles straight into the stage buffer by LDS-DMA (it is not being read: the previous
+    // reader of this buffer finished before the last barrier)
+    char* base = smem + ((j & 1) * KS + sp) * SB;
+    GldsTile<D, kTile>::load(P.q + (long)b * T * P.q_stride + hq * D, P.q_stride, t * kTile, base, wv, lane);
+    GldsTile<D, kTile>::load(P.dout + (long)b * T * P.do_stride + hq * D, P.do_stride, t * kTile, base + TB, wv, lane);
     if (stid < kTile) {   // row constants, loaded straight into the S / dP accumulators
       vl = -P.lse[bq * T + t * kTile + stid] * inv_scale;
       vd = -P.delta[bq * T + t * kTile + stid] * inv_s;
@@ -459,8 +462,6 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     tile_of(j, g, t);
     if (t >= nT) return;
     char* base = smem + ((j & 1) * KS + sp) * SB;
-    lq.store(base, stid);
-    ldo.store(base + TB, stid);
     float* f = reinterpret_cast<float*>(base + 2 * TB);
     if (stid < kTile) {
       f[stid] = vl;
@@ -497,16 +498,24 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
           dp[4 * g4 + 0] = Dl.x; dp[4 * g4 + 1] = Dl.y; dp[4 * g4 + 2] = Dl.z; dp[4 * g4 + 3] = Dl.w;
         }
       }
-      bfx8 qa[D / 16], da[D / 16];     // all fragments first: one lgkmcnt wait, not one per MFMA
+      if constexpr (D == 128) {        // 1 wave / SIMD: all fragments first (one lgkmcnt wait)
+        bfx8 qa[D / 16], da[D / 16];
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        qa[s] = row_frag<D>(qt, 32 * mm + r, 2 * s + h);
-        da[s] = row_frag<D>(dt_, 32 * mm + r, 2 * s + h);
-      }
+        for (int s = 0; s < D / 16; ++s) {
+          qa[s] = row_frag<D>(qt, 32 * mm + r, 2 * s + h);
+          da[s] = row_frag<D>(dt_, 32 * mm + r, 2 * s + h);
+        }
 #pragma unroll
-      for (int s = 0; s < D / 16; ++s) {
-        sa = mfma32(qa[s], kf[s], sa);
-        dp = mfma32(da[s], vf[s], dp);
+        for (int s = 0; s < D / 16; ++s) {
+          sa = mfma32(qa[s], kf[s], sa);
+          dp = mfma32(da[s], vf[s], dp);
+        }
+      } else {                         // several waves / SIMD hide the reads; keep registers low
+#pragma unroll
+        for (int s = 0; s < D / 16; ++s) {
+          sa = mfma32(row_frag<D>(qt, 32 * mm + r, 2 * s + h), kf[s], sa);
+          dp = mfma32(row_frag<D>(dt_, 32 * mm + r, 2 * s + h), vf[s], dp);
+        }
       }
     };
     auto softmax = [&](int mm, const f32x16& sa, const f32x16& dp, bool diag, f32x16& pd, f32x16& ds) {
@@ -541,25 +550,20 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     auto accum = [&](int mm, const f32x16& pd, const f32x16& ds) {
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bfx8 ta[NACC], tq[NACC];
-#pragma unroll
-        for (int d_ = 0; d_ < NACC; ++d_) {
-          ta[d_] = tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane);
-          tq[d_] = tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane);
-        }
         const bfx8 pf = pack_frag<D>(pd, s2);
         const bfx8 sf = pack_frag<D>(ds, s2);
 #pragma unroll
         for (int d_ = 0; d_ < NACC; ++d_) {
-          dv[d_] = mfma32(ta[d_], pf, dv[d_]);
-          dk[d_] = mfma32(tq[d_], sf, dk[d_]);
+          dv[d_] = mfma32(tr_frag<D>(dt_, 32 * mm + 16 * s2, d_ * 32, lane), pf, dv[d_]);
+          dk[d_] = mfma32(tr_frag<D>(qt, 32 * mm + 16 * s2, d_ * 32, lane), sf, dk[d_]);
         }
       }
     };
     if (t < nT) {
-      if (!CAUSAL || t * kTile >= k0 + 31) {
-        // full tile (no mask): both sub-tiles' S/dP first, so the second pair's MFMAs overlap the
-        // first sub-tile's softmax, and its dV/dK MFMAs overlap the second softmax
+      if (D == 128 && (!CAUSAL || t * kTile >= k0 + 31)) {
+        // full tile (no mask) at 1 wave / SIMD: both sub-tiles' S/dP first, so the second pair's
+        // MFMAs overlap the first sub-tile's softmax, and its dV/dK MFMAs overlap the second
+        // softmax (at D = 64 more waves per SIMD do that, and the registers are needed for them)
         f32x16 sa0, dp0, sa1, dp1, pd, ds;
         sdp(0, sa0, dp0);
         sdp(1, sa1, dp1);
@@ -582,10 +586,11 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     if (j + 1 < njobs) store(j + 1);
     __syncthreads();
   }
-  if constexpr (KS == 2) {
+  if constexpr (KS > 1) {      // splits 1..KS-1 -> LDS -> split 0
     constexpr int NF = 2 * 16 * NACC;
-    float* red = reinterpret_cast<float*>(smem) + kw * NF * 64 + lane;
-    if (sp == 1) {
+    float* red0 = reinterpret_cast<float*>(smem) + kw * NF * 64 + lane;
+    if (sp > 0) {
+      float* red = red0 + (sp - 1) * 4 * NF * 64;
 #pragma unroll
       for (int dt = 0; dt < NACC; ++dt)
 #pragma unroll
@@ -595,14 +600,16 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
         }
     }
     __syncthreads();
-    if (sp == 1) return;
+    if (sp > 0) return;
 #pragma unroll
-    for (int dt = 0; dt < NACC; ++dt)
+    for (int o = 0; o < KS - 1; ++o)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        dk[dt][i] += red[(16 * dt + i) * 64];
-        dv[dt][i] += red[(16 * (NACC + dt) + i) * 64];
-      }
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          dk[dt][i] += red0[o * 4 * NF * 64 + (16 * dt + i) * 64];
+          dv[dt][i] += red0[o * 4 * NF * 64 + (16 * (NACC + dt) + i) * 64];
+        }
   }
   const float s_drop = DROP ? P.drop_scale : 1.f;
   bf16_t* dkrow = P.out + ((long)b * T + key) * P.out_stride + hk * D;
