@@ -575,7 +575,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
 #pragma unroll
         for (int mm = 0; mm < 2; ++mm) {
           const int qb = t * kTile + 32 * mm;
-          if (qb + 31 < k0) continue;   // every query < every key of this wave
+          if (CAUSAL && qb + 31 < k0) continue;   // every query < every key of this wave
           f32x16 sa, dp, pd, ds;
           sdp(mm, sa, dp);
           softmax(mm, sa, dp, qb < k0 + 31, pd, ds);
