@@ -64,6 +64,10 @@ class TinyGPTBlock(nn.Module):
 
 
 # ============================================================================ fused Functions
+# DLTB_MASK_STREAM=1: generate the attention dropout mask on a side stream, concurrent with LN1 + QKV
+_MASK_STREAM = __import__("os").environ.get("DLTB_MASK_STREAM", "0") == "1"
+
+
 class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, idx, model):
@@ -99,7 +103,7 @@ class _BlockFn(torch.autograd.Function):
         cfg = model.cfg
         H, d = cfg.n_head, cfg.n_embd
         p = model.drop_p
-        par = GradStreams(x.device)
+        par = GradStreams(x.device, enabled=_MASK_STREAM or None)
         amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x, par)   # overlaps LN1 + QKV GEMM
         _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False)
         qkv = F_.linear_fwd(h1, win, bin_)
