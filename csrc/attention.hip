@@ -189,6 +189,15 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
   if (causal) qb = nqb - 1 - qb;
 }
 
+template <int D>
+constexpr int fwd_ks() { return D == 64 ? 3 : 2; }   // KS = 4 at D = 64 spills (128 VGPRs) and is slower
+template <int D>
+constexpr int fwd_nst() { return D == 64 ? 3 : 2; }  // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
+template <int D>
+constexpr int fwd_stage_bytes() { return 2 * kTile * D * 2 + 1024; }   // K, V, dropout words of 4 waves
+template <int D>
+constexpr int fwd_smem_bytes() { return fwd_nst<D>() * fwd_ks<D>() * fwd_stage_bytes<D>(); }
+
 template <int D, bool CAUSAL, bool DROP, int KS>
 __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
@@ -216,13 +225,25 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   const uint32_t* mrow = DROP ? P.mask + ((long)bh * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
 
+  // NST-deep ring of (K, V, dropout-word) stages per key split, filled by compiler-invisible
+  // LDS-DMA; a counted vmcnt retires only the stage about to be read and a raw s_barrier
+  // publishes it, so NST-2 later stages stay in flight across the barrier.
+  constexpr int NST = fwd_nst<D>();
+  constexpr int SB = fwd_stage_bytes<D>();
+  constexpr int GL = 2 * GldsTile<D, kTile>::NI + (DROP ? 1 : 0);   // DMA instructions per stage
   const int wv = __builtin_amdgcn_readfirstlane(qw);
-  if (sp < nt) {
-    GldsTile<D, kTile>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
-    GldsTile<D, kTile>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
-  }
-  uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
-  __syncthreads();
+  auto stage_ptr = [&](int it) { return smem + ((it % NST) * KS + sp) * SB; };
+  auto issue = [&](int it) {
+    const int t = it * KS + sp;
+    if (it >= nit || t >= nt) return;
+    char* st = stage_ptr(it);
+    GldsTile<D, kTile, true>::load(kbase, P.k_stride, t * kTile, st, wv, lane);
+    GldsTile<D, kTile, true>::load(vbase, P.v_stride, t * kTile, st + TB, wv, lane);
+    if (DROP) glds4_asm(mrow + (long)t * 2 * T, st + 2 * TB + wv * 256);
+  };
+  wait_vm<0>();        // Q fragments landed: no compiler vmcnt wait for them inside the loop
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i) issue(i);
 
   f32x16 oacc[NACC];
 #pragma unroll
@@ -231,16 +252,15 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
 
   for (int it = 0; it < nit; ++it) {
     const int t = it * KS + sp;
-    const char* kt = smem + ((it & 1) * KS + sp) * 2 * TB;
+    // stage it+1 (issued only if its tile exists for this split) may stay in flight
+    static_assert(NST <= 3, "the counted wait below assumes at most one later stage in flight");
+    if (NST > 2 && it + 1 < nit && (it + 1) * KS + sp < nt) wait_vm<(NST > 2 ? GL : 0)>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    issue(it + NST - 1);                         // refills the buffer read in iteration it - 1
+    const char* kt = stage_ptr(it);
     const char* vt = kt + TB;
-    const uint32_t mw = mw_next;
-    const int tn = t + KS;
-    if (tn < nt) {
-      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
-      GldsTile<D, kTile>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
-      GldsTile<D, kTile>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
-      if (DROP) mw_next = mrow[(long)tn * 2 * T];
-    }
+    const uint32_t mw = DROP ? *reinterpret_cast<const uint32_t*>(kt + 2 * TB + wv * 256 + lane * 4) : 0u;
     const int kv0 = t * kTile;
     if (t < nt && (!CAUSAL || kv0 <= q0 + 31)) {
       f32x16 sacc[2];
@@ -290,11 +310,11 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
         }
       }
     }
-    __syncthreads();
   }
+  __syncthreads();              // all LDS reads done before the ring is reused for the merge
   if constexpr (KS > 1) {      // merge the key splits: splits 1..KS-1 -> LDS -> split 0
     constexpr int NF = 16 * NACC + 2;
-    static_assert((KS - 1) * 4 * NF * 64 * 4 <= 4 * KS * kTile * D * 2, "merge buffer exceeds the LDS ring");
+    static_assert((KS - 1) * 4 * NF * 64 * 4 <= NST * KS * SB, "merge buffer exceeds the LDS ring");
     float* red0 = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
     if (sp > 0) {
       float* red = red0 + (sp - 1) * 4 * NF * 64;
@@ -328,10 +348,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   if (h == 0) P.lse[((long)b * P.Hq + hq) * T + qi] = (m + __log2f(l)) * 0.69314718055994531f;
 }
 
-template <int D>
-constexpr int fwd_ks() { return D == 64 ? 3 : 2; }   // KS = 4 at D = 64 spills (128 VGPRs) and is slower
-template <int D>
-constexpr int fwd_smem_bytes() { return 4 * fwd_ks<D>() * kTile * D * 2; }
+
 
 // =============================================================================== backward prep
 // delta[b, h, t] = sum_d dO[b,t,h,d] * O[b,t,h,d]

@@ -45,13 +45,6 @@ struct Geo {
   static constexpr int STAGE = A_BYTES + B_BYTES;
 };
 
-// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt / lgkmcnt at max)
-template <int N>
-DLTB_DEV void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-
 template <int BM, int BN, bool TN, int NSTAGE>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   using G = Geo<BM, BN, TN>;

@@ -74,6 +74,24 @@ DLTB_DEV void glds16_asm(const void* gsrc, const void* lds_dst) {
                : "memory");
 }
 
+// 4-byte LDS-DMA from inline asm (one dword per lane -> 256 contiguous LDS bytes per wave).
+DLTB_DEV void glds4_asm(const void* gsrc, const void* lds_dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt / lgkmcnt at max)
+template <int N>
+DLTB_DEV void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
 template <int D, int ROWS, bool ASM = false>
 struct GldsTile {
   static constexpr int CH = D / 8;
