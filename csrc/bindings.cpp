@@ -586,7 +586,7 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K, bool tn, int64_t cfg) {
 }
 
 Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const optional<Tensor>& bias,
-            bool tn, bool accumulate, int64_t splits, int64_t cfg) {
+            bool tn, bool accumulate, int64_t splits, int64_t cfg, int64_t pf, int64_t gm) {
   check_bf16(a, "a");
   check_bf16(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm: 2-D, inner dim contiguous");
@@ -617,7 +617,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const
   if (splits > 1) part = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
   dltb_gemm(a.data_ptr(), b.data_ptr(), c.data_ptr(), bp, splits > 1 ? part.data_ptr<float>() : nullptr,
             a.stride(0), b.stride(0), c.stride(0), (int)M, (int)N, (int)K, tn, accumulate ? 1 : 0,
-            (int)splits, (int)cfg, cur_stream());
+            (int)splits, (int)cfg, (int)pf, (int)gm, cur_stream());
   return c;
 }
 
@@ -650,7 +650,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
   m.def("colpart", &colpart);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias"), py::arg("tn"),
+        py::arg("accumulate"), py::arg("splits") = 1, py::arg("cfg") = 0, py::arg("pf") = 0, py::arg("gm") = 1);
   m.def("gemm_supported", &gemm_supported);
   m.def("transpose_into", &transpose_into);
   m.def("colreduce_multi", &colreduce_multi);

@@ -34,6 +34,8 @@ struct GemmArgs {
   int M, N, K;
   int accumulate;
   int ksplit;           // K range per split (multiple of kBK)
+  int pf;               // L2 prefetch distance in k-steps (PF kernels)
+  int gm;               // tile order: groups of gm row-blocks (each XCD's run covers gm x (run / gm) tiles)
 };
 
 // tile image geometry: NT -> rows = m (or n), 64 k per row (D = 64 image, BM rows);
@@ -45,7 +47,7 @@ struct Geo {
   static constexpr int STAGE = A_BYTES + B_BYTES;
 };
 
-template <int BM, int BN, bool TN, int NSTAGE>
+template <int BM, int BN, bool TN, int NSTAGE, bool PF>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   using G = Geo<BM, BN, TN>;
   constexpr int WM = BM / 2, WN = BN / 2;          // wave tile
@@ -62,11 +64,39 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   L -= split * tiles;
   int idx = L;
   if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
-  const int m0 = (idx / tiles_n) * BM, n0 = (idx % tiles_n) * BN;
+  int mb = idx / tiles_n, nb = idx % tiles_n;
+  const int tiles_m = g.M / BM;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {          // grouped order: gm row-blocks x all column-blocks
+    const int grp = idx / (g.gm * tiles_n), in = idx % (g.gm * tiles_n);
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
   const int kbeg = split * g.ksplit;
   const int nk = min(g.ksplit, g.K - kbeg) / kBK;
 
+  // L2 prefetch of k-step kt + pf: one 4-byte LDS-DMA per 128-byte line of the stage (BM + BN lines),
+  // landing in a scratch LDS slot.  The XCD's L2 then already holds the lines when the real stage is
+  // issued, so the ring only has to cover L2 latency, not the Infinity-Cache latency of first touch.
+  constexpr int NPF = PF ? (BM + BN + 255) / 256 : 0;
+  auto prefetch = [&](int kt) {
+    const int kp = kbeg + min(kt + g.pf, nk - 1) * kBK;
+#pragma unroll
+    for (int i = 0; i < NPF; ++i) {
+      int t = (i * 256 + tid) % (BM + BN);
+      const bf16_t* src;
+      if constexpr (!TN) {
+        src = t < BM ? g.a + (long)(m0 + t) * g.lda + kp : g.b + (long)(n0 + t - BM) * g.ldb + kp;
+      } else {
+        if (t < BM) src = g.a + (long)(kp + t / (BM / 64)) * g.lda + m0 + (t % (BM / 64)) * 64;
+        else { t -= BM; src = g.b + (long)(kp + t / (BN / 64)) * g.ldb + n0 + (t % (BN / 64)) * 64; }
+      }
+      glds4_asm(src, smem + NSTAGE * G::STAGE + wv * 256);
+    }
+  };
+
   auto load_stage = [&](int kt, int st) {
+    if constexpr (PF) prefetch(kt);
     char* sa = smem + st * G::STAGE;
     char* sb = sa + G::A_BYTES;
     const int k0 = kbeg + kt * kBK;
@@ -88,8 +118,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   // NSTAGE-deep LDS ring filled by LDS-DMA.  Each wave issues GLDS wave-instructions per stage;
   // a COUNTED vmcnt (not __syncthreads' vmcnt(0)) retires only the stage about to be read, so the
   // next NSTAGE-2 stages stay in flight across the raw s_barrier.
-  constexpr int GLDS = TN ? (GldsTile<BM, kBK>::NI + GldsTile<BN, kBK>::NI)
-                          : (GldsTile<64, BM>::NI + GldsTile<64, BN>::NI);
+  constexpr int GLDS = NPF + (TN ? (GldsTile<BM, kBK>::NI + GldsTile<BN, kBK>::NI)
+                                : (GldsTile<64, BM>::NI + GldsTile<64, BN>::NI));
 #pragma unroll
   for (int st = 0; st < NSTAGE - 1; ++st)
     if (st < nk) load_stage(st, st);
@@ -183,32 +213,50 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int splits
   }
 }
 
-template <int BM, int BN, bool TN>
-void launch_t(const GemmArgs& g, int splits, hipStream_t st) {
+template <int BM, int BN, bool TN, bool PF>
+void launch_pf(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int NSTAGE = Geo<BM, BN, TN>::STAGE <= 32768 ? 4 : 3;   // <= 128 KiB of LDS ring
-  constexpr int smem = NSTAGE * Geo<BM, BN, TN>::STAGE;
+  constexpr int smem = NSTAGE * Geo<BM, BN, TN>::STAGE + (PF ? 1024 : 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, TN, NSTAGE>,
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<BM, BN, TN, NSTAGE, PF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int tiles = (g.M / BM) * (g.N / BN);
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, TN, NSTAGE>), dim3(tiles * splits), dim3(256), smem, st, g);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, TN, NSTAGE, PF>), dim3(tiles * splits), dim3(256), smem, st, g);
+}
+
+template <int BM, int BN, bool TN>
+void launch_t(const GemmArgs& g, int splits, hipStream_t st) {
+  if (g.pf > 0) launch_pf<BM, BN, TN, true>(g, splits, st);
+  else launch_pf<BM, BN, TN, false>(g, splits, st);
 }
 
 }  // namespace
 
-// tile config: 0 = 128x128, 1 = 256x128 (BM 256), 2 = 128x256 (BN 256)
+// tile configs (BM x BN): 0 = 128x128, 1 = 256x128, 2 = 128x256, 3 = 128x64, 4 = 64x128, 5 = 64x64
+static void cfg_tile(int cfg, int& BM, int& BN) {
+  static const int t[6][2] = {{128, 128}, {256, 128}, {128, 256}, {128, 64}, {64, 128}, {64, 64}};
+  if (cfg < 0 || cfg > 5) cfg = 0;
+  BM = t[cfg][0];
+  BN = t[cfg][1];
+}
+
 bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg) {
-  if (tn && cfg != 0) return false;      // TN images are 128-element rows (swizzle of mfma_tiles.h)
-  const int BM = cfg == 1 ? 256 : 128, BN = cfg == 2 ? 256 : 128;
+  if (cfg < 0 || cfg > 5) return false;
+  int BM, BN;
+  cfg_tile(cfg, BM, BN);
+  if (tn && (BM > 128 || BN > 128)) return false;   // TN images are <= 128-element rows (mfma_tiles.h swizzle)
   return M % BM == 0 && N % BN == 0 && K % kBK == 0 && M > 0 && N > 0 && K > 0;
 }
 
 int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
-              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, hipStream_t st) {
+              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
+              hipStream_t st) {
   GemmArgs g{};
+  g.pf = pf;
+  g.gm = gm;
   g.a = (const bf16_t*)a;
   g.b = (const bf16_t*)b;
   g.c = (bf16_t*)c;
@@ -232,9 +280,14 @@ int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* pa
     if (tn) launch_t<BM, BN, true>(g, splits, st);                  \
     else launch_t<BM, BN, false>(g, splits, st);                    \
   } while (0)
-  if (cfg == 1 && !tn) launch_t<256, 128, false>(g, splits, st);
-  else if (cfg == 2 && !tn) launch_t<128, 256, false>(g, splits, st);
-  else DLTB_G(128, 128);
+  switch (cfg) {
+    case 1: launch_t<256, 128, false>(g, splits, st); break;
+    case 2: launch_t<128, 256, false>(g, splits, st); break;
+    case 3: DLTB_G(128, 64); break;
+    case 4: DLTB_G(64, 128); break;
+    case 5: DLTB_G(64, 64); break;
+    default: DLTB_G(128, 128); break;
+  }
 #undef DLTB_G
   if (splits > 1) {
     long total4 = (long)M * N / 4;

@@ -109,4 +109,4 @@ void dltb_colreduce_multi(const DltbColRedSeg* segs, int nseg, hipStream_t st);
 // ---- gemm.hip: C[M,N] = A B (+bias) (+C); NT: A [M][K], B [N][K]; TN: A [K][M], B [K][N]
 bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg);
 int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
-              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, hipStream_t st);
+              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm, hipStream_t st);

@@ -50,8 +50,12 @@ def main():
     ap.add_argument("--model", default="A")
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--layouts", action="store_true", help="also time the NT-form alternatives")
+    ap.add_argument("--best", action="store_true", help="with --dltb: print only the fastest dltb config per product")
+    ap.add_argument("--probe", action="store_true", help="single-workgroup K sweep of each dltb tile config")
     ap.add_argument("--dltb", action="store_true", help="also time the dltb MFMA GEMM (tile configs x split-K)")
     a = ap.parse_args()
+    if a.probe:
+        return probe(a.iters)
     M, lst = shapes(a.model)
     dt = torch.bfloat16
     rows, total = [], 0.0
@@ -71,14 +75,17 @@ def main():
         if a.dltb:
             from dltb.ops._ext import ext
             C = ext()
-            for cfg in (0, 1, 2):
-                for sp in (1, 2, 4):
-                    if C.gemm_supported(M, N, K, False, cfg):
-                        kinds.append((f"fwd[c{cfg}s{sp}]", lambda cfg=cfg, sp=sp: C.gemm(x, w, y, None, False, False, sp, cfg)))
-                    if C.gemm_supported(M, K, N, False, cfg):
-                        kinds.append((f"dgT[c{cfg}s{sp}]", lambda cfg=cfg, sp=sp: C.gemm(dy, wT, dx, None, False, False, sp, cfg)))
-                    if C.gemm_supported(N, K, M, True, cfg):
-                        kinds.append((f"wg[c{cfg}s{sp}]", lambda cfg=cfg, sp=sp: C.gemm(dy, x, dw, None, True, False, sp, cfg)))
+            for cfg in range(6):
+                for sp in (1, 2):
+                    for pf in ((0, 2, 4, 8) if sp == 1 else (0,)):
+                        for gm in ((1, 2, 4, 8) if sp == 1 else (1,)):
+                            tag = f"c{cfg}s{sp}p{pf}g{gm}"
+                            if C.gemm_supported(M, N, K, False, cfg):
+                                kinds.append((f"fwd[{tag}]", lambda cfg=cfg, sp=sp, pf=pf, gm=gm: C.gemm(x, w, y, None, False, False, sp, cfg, pf, gm)))
+                            if C.gemm_supported(M, K, N, False, cfg):
+                                kinds.append((f"dgT[{tag}]", lambda cfg=cfg, sp=sp, pf=pf, gm=gm: C.gemm(dy, wT, dx, None, False, False, sp, cfg, pf, gm)))
+                            if C.gemm_supported(N, K, M, True, cfg):
+                                kinds.append((f"wg[{tag}]", lambda cfg=cfg, sp=sp, pf=pf, gm=gm: C.gemm(dy, x, dw, None, True, False, sp, cfg, pf, gm)))
         if a.layouts:
             kinds += [("dgradT", lambda: torch.mm(dy, wT.t(), out=dx)),     # W^T cached: NT form
                       ("wgradT", lambda: torch.mm(dyT, xT.t(), out=dw))]    # activations transposed
@@ -87,10 +94,40 @@ def main():
             if kind in ("fwd", "dgrad", "wgrad"):
                 total += us * reps
             rows.append((name, kind, M, N, K, reps, us, fl / us / 1e6))
+    if a.best:
+        best = {}
+        for r in rows:
+            key = (r[0], r[1][:3] if "[" in r[1] else r[1])
+            if "[" in r[1] and (key not in best or r[6] < best[key][6]):
+                best[key] = r
+        rows = [r for r in rows if "[" not in r[1]] + list(best.values())
     for name, kind, m, n, k, reps, us, tf in rows:
         print(f"{name:8s} {kind:6s} M{m:6d} N{n:6d} K{k:6d} x{reps:3d} {us:8.1f} us {tf:7.1f} TF/s "
               f"{100 * us * reps / total:5.1f}%")
     print(f"total GEMM time per step (1 micro-batch): {total / 1e3:.3f} ms")
+
+
+def probe(iters):
+    """One workgroup (M = BM, N = BN) over growing K: per-64-deep-k-step cycles of the pipeline."""
+    from dltb.ops._ext import ext
+    C = ext()
+    tiles = [(128, 128), (256, 128), (128, 256), (128, 64), (64, 128), (64, 64)]
+    for cfg, (bm, bn) in enumerate(tiles):
+        for tn in (False, True):
+            if not C.gemm_supported(bm, bn, 1024, tn, cfg):
+                continue
+            out = []
+            for K in (1024, 4096, 16384):
+                a = torch.randn((K, bm) if tn else (bm, K), device="cuda", dtype=torch.bfloat16)
+                b = torch.randn((K, bn) if tn else (bn, K), device="cuda", dtype=torch.bfloat16)
+                c = torch.empty(bm, bn, device="cuda", dtype=torch.bfloat16)
+                us = timeit(lambda: C.gemm(a, b, c, None, tn, False, 1, cfg), iters)
+                out.append((K, us))
+            (k0, t0), (k1, t1) = out[1], out[2]
+            per = (t1 - t0) / ((k1 - k0) / 64) * 2.4e3      # cycles per k-step at 2.4 GHz
+            mf = (bm // 2 // 32) * (bn // 2 // 32) * 4 * 32  # MFMA cycles per k-step per wave
+            print(f"cfg{cfg} {bm}x{bn} {'TN' if tn else 'NT'}: " + "  ".join(f"K{k}={t:.1f}us" for k, t in out)
+                  + f"  -> {per:.0f} cyc/k-step (MFMA-bound {mf})")
 
 
 if __name__ == "__main__":

@@ -173,8 +173,11 @@ def test_sumsq_is_deterministic():
 
 @pytest.mark.parametrize("tn", [False, True])
 @pytest.mark.parametrize("M,N,K,cfg,splits", [(256, 384, 512, 0, 1), (512, 256, 1024, 0, 4),
-                                               (512, 256, 256, 1, 1), (256, 512, 192, 2, 2)])
-def test_gemm(tn, M, N, K, cfg, splits):
+                                               (512, 256, 256, 1, 1), (256, 512, 192, 2, 2),
+                                               (256, 192, 512, 3, 1), (192, 256, 320, 4, 2),
+                                               (192, 320, 256, 5, 1)])
+@pytest.mark.parametrize("pf,gm", [(0, 1), (3, 2)])
+def test_gemm(tn, M, N, K, cfg, splits, pf, gm):
     """dltb GEMM (NT: a[M,K] b[N,K]; TN: a[K,M] b[K,N]) vs fp32 torch, incl. bias / accumulate /
     split-K and row-strided operand views."""
     C_ = ext()
@@ -189,11 +192,11 @@ def test_gemm(tn, M, N, K, cfg, splits):
         a, b = a_full[:, :K], b_full
         ref32 = a.float() @ b.float().t()
     bias = rnd(N)
-    out = C_.gemm(a, b, None, bias, tn, False, splits, cfg)
+    out = C_.gemm(a, b, None, bias, tn, False, splits, cfg, pf, gm)
     close(out, ref32 + bias.float(), 0.1, 2e-2, "gemm + bias")
     prev = rnd(M, N)
     acc = prev.clone()
-    C_.gemm(a, b, acc, None, tn, True, splits, cfg)
+    C_.gemm(a, b, acc, None, tn, True, splits, cfg, pf, gm)
     close(acc, ref32 + prev.float(), 0.1, 2e-2, "gemm accumulate")
 
 
