@@ -29,6 +29,7 @@ from .models import build_model, get_model_config
 from .parallel.checkpoint import export_consolidated, load_checkpoint, save_checkpoint
 from .parallel.graphs import GraphedStep, graphs_enabled
 from .ops._ext import available as ext_available, so_path
+from .comm import describe as comm_describe
 from .parallel import STRATEGIES, engine_config, make_engine
 from .parallel.strategy import default_config_path, load_deepspeed_config, load_fsdp_config
 from .results import make_record, print_markers, print_result, write_result
@@ -157,6 +158,7 @@ def train(args):
             if step == args.warmup_steps:
                 barrier()
                 sync()
+                engine.comm.reset_stats()     # wire accounting over the timed steps only
                 t_start = time.perf_counter()
                 if args.profile and is_main:
                     from torch.profiler import ProfilerActivity, profile
@@ -234,6 +236,12 @@ def train(args):
             "optimizer_steps": engine.opt_steps, "last_lr": engine.last_lr,
             "grad_norm": float(engine.grad_norm.item()) if engine.grad_norm is not None else None,
             "comm_bytes_per_step_per_gpu": engine.comm_bytes_per_step,
+            # measured by the comm layer (host-issued calls; graph replays issue none from Python)
+            "comm_wire_bytes_per_step_measured": (engine.comm.wire_bytes() / timed
+                                                  if timed > 0 and not (runner is not None and runner.graphs
+                                                                        and not runner.disabled) else None),
+            "comm_ops_timed": {k: dict(v) for k, v in engine.comm.stats.items()},
+            "comm_topology": comm_describe(world) if (is_main and device.type == "cuda") else None,
             "memory": engine.memory_report(),
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
             "accum_semantics": args.accum_semantics, "dtype": args.dtype, "data_loader": args.data_loader,

@@ -19,8 +19,8 @@ from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
-import torch.distributed as dist
 
+from ..comm import Comm
 from ..ops._ext import ext
 from ..ops.rng import StepSeed
 from ..optim.sched import build_scheduler
@@ -60,11 +60,8 @@ class Engine(ParamRuntime):
         self.cfg = cfg
         self.device = torch.device(device)
         self.group = group
-        if dist.is_available() and dist.is_initialized():
-            self.world = dist.get_world_size(group)
-            self.rank = dist.get_rank(group)
-        else:
-            self.world, self.rank = 1, 0
+        self.comm = Comm(group)          # every collective of the engine goes through this
+        self.world, self.rank = self.comm.world, self.comm.rank
         self.accum = max(1, int(cfg.grad_accum))
         self.compute_dtype = cfg.compute_dtype if self.device.type == "cuda" else torch.float32
         self.seed = StepSeed(cfg.seed, self.rank, self.device)
@@ -74,7 +71,6 @@ class Engine(ParamRuntime):
         self._is_boundary = self.accum == 1
         self._window_pos = 0
         self._written = {}
-        self._works = []
         self.last_lr = None
         self.grad_norm = None
         self._norm_sq = torch.zeros(1, device=self.device, dtype=torch.float32)
@@ -206,9 +202,7 @@ class Engine(ParamRuntime):
 
     # ------------------------------------------------------------------ helpers
     def _wait_works(self):
-        for w in self._works:
-            w.wait()
-        self._works.clear()
+        self.comm.wait_all()
 
     def _sumsq_into(self, t: torch.Tensor, out: torch.Tensor):
         if t.is_cuda:
@@ -227,7 +221,7 @@ class Engine(ParamRuntime):
         for g in grads:
             self._sumsq_into(g, self._norm_sq)
         if sharded and self.world > 1:
-            dist.all_reduce(self._norm_sq, group=self.group)
+            self.comm.all_reduce(self._norm_sq, async_op=False)
         if self.device.type == "cuda":
             if self.grad_norm is None:
                 self.grad_norm = torch.zeros(1, device=self.device)

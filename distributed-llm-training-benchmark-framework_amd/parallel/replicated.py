@@ -21,7 +21,6 @@ DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
 import os
 
 import torch
-import torch.distributed as dist
 
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
@@ -136,11 +135,9 @@ class ReplicatedEngine(Engine):
         bk = self.layout.buckets[b]
         g = self.flat_grad[bk.start:bk.end]
         if self.stage == 0:
-            w = dist.all_reduce(g, group=self.group, async_op=True)
+            self.comm.all_reduce(g)
         else:
-            out = self.rs_out[bk.owner_start:bk.owner_start + bk.chunk]
-            w = dist.reduce_scatter_tensor(out, g, group=self.group, async_op=True)
-        self._works.append(w)
+            self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g)
         self._launched[b] = True
 
     # ------------------------------------------------------------------ step lifecycle
@@ -185,7 +182,7 @@ class ReplicatedEngine(Engine):
             bk = self.layout.buckets[b]
             full = self.flat_param[bk.start:bk.end]
             mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
-            self._ag_pending[b] = dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+            self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
 
     def _wait_param_gathers(self):
         for w in self._ag_pending.values():
@@ -199,7 +196,7 @@ class ReplicatedEngine(Engine):
             for bk in self.layout.buckets:
                 full = self.flat_param[bk.start:bk.end]
                 mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
-                self._works.append(dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True))
+                self.comm.all_gather(full, mine)
             self._wait_works()
 
     def _after_param_load(self):
@@ -208,7 +205,7 @@ class ReplicatedEngine(Engine):
             for bk in self.layout.buckets:
                 full = self.flat_param[bk.start:bk.end]
                 mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
-                dist.all_gather_into_tensor(full, mine, group=self.group)
+                self.comm.all_gather(full, mine, async_op=False)
 
     # ------------------------------------------------------------------ introspection
     def memory_report(self):
@@ -225,7 +222,7 @@ class ReplicatedEngine(Engine):
             full = torch.zeros(self.layout.total, dtype=torch.float32, device=self.device)
             for ostart, ln, fstart in owner_segments(self.layout, self.rank):
                 full[fstart:fstart + ln] = self.opt.master[ostart:ostart + ln]
-            dist.all_reduce(full, group=self.group)
+            self.comm.all_reduce(full, async_op=False)
         elif self.stage >= 1:
             full = torch.zeros(self.layout.total, dtype=torch.float32, device=self.device)
             for ostart, ln, fstart in owner_segments(self.layout, self.rank):

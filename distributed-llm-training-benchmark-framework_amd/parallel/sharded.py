@@ -24,7 +24,6 @@ MI355X-native design on ``torch.distributed`` (RCCL over xGMI):
   the bf16 shard is written in place and becomes the next all-gather's input.
 """
 import torch
-import torch.distributed as dist
 
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
@@ -165,7 +164,7 @@ class ShardedEngine(Engine):
             g.full = g.shard
             return
         g.full = torch.empty(g.total, dtype=self.shard_buf.dtype, device=self.device)
-        g.work = dist.all_gather_into_tensor(g.full, g.shard, group=self.group, async_op=True)
+        g.work = self.comm.all_gather(g.full, g.shard, track=False)
 
     def _ensure(self, g):
         self._launch_gather(g)
@@ -266,7 +265,7 @@ class ShardedEngine(Engine):
             return
         if self.world > 1:
             out = self.rs_out[g.owner_start:g.owner_start + g.chunk]
-            self._works.append(dist.reduce_scatter_tensor(out, g.grad, group=self.group, async_op=True))
+            self.comm.reduce_scatter(out, g.grad)
             self._held_grads.append(g.grad)
         g.grad = None
 
@@ -275,8 +274,7 @@ class ShardedEngine(Engine):
         if pc == 0:
             return
         if self.world > 1:
-            self._works.append(dist.reduce_scatter_tensor(self.rs_out[:pc], self.p_grad, group=self.group,
-                                                          async_op=True))
+            self.comm.reduce_scatter(self.rs_out[:pc], self.p_grad)
         else:
             self.rs_out[:pc].copy_(self.p_grad)
 
@@ -322,7 +320,7 @@ class ShardedEngine(Engine):
         pc = self.p_layout.owner_numel
         if pc and self.world > 1:
             mine = self.p_flat[self.rank * pc:(self.rank + 1) * pc]
-            dist.all_gather_into_tensor(self.p_flat, mine, group=self.group)
+            self.comm.all_gather(self.p_flat, mine, async_op=False)
 
     def _after_param_load(self):
         for grp in self.groups:                   # gathered copies (if any) are stale
@@ -330,7 +328,7 @@ class ShardedEngine(Engine):
         pc = self.p_layout.owner_numel
         if pc and self.world > 1:
             mine = self.p_flat[self.rank * pc:(self.rank + 1) * pc]
-            dist.all_gather_into_tensor(self.p_flat, mine, group=self.group)
+            self.comm.all_gather(self.p_flat, mine, async_op=False)
 
     # ------------------------------------------------------------------ introspection
     def memory_report(self):
@@ -347,14 +345,14 @@ class ShardedEngine(Engine):
             pfull = torch.zeros(self.p_layout.total, dtype=torch.float32, device=self.device)
             pfull[self.rank * pc:(self.rank + 1) * pc] = self.opt.master[:pc]
             if self.world > 1:
-                dist.all_reduce(pfull, group=self.group)
+                self.comm.all_reduce(pfull, async_op=False)
             for s in self.p_layout.slots.values():
                 out[s.unit.names[s.index]] = pfull[s.offset:s.offset + s.numel].view(s.shape).clone()
         for g in self.groups:
             gfull = torch.zeros(g.total, dtype=torch.float32, device=self.device)
             gfull[self.rank * g.chunk:(self.rank + 1) * g.chunk] = self.opt.master[g.owner_start:g.owner_start + g.chunk]
             if self.world > 1:
-                dist.all_reduce(gfull, group=self.group)
+                self.comm.all_reduce(gfull, async_op=False)
             for s in g.layout.slots.values():
                 out[s.unit.names[s.index]] = gfull[s.offset:s.offset + s.numel].view(s.shape).clone()
         return out

@@ -1,0 +1,106 @@
+"""Comm layer (dltb/comm): collectives over gloo at world size 2, wire accounting, the single-process
+no-op path, and the xGMI topology / bucket-size model."""
+import os
+import socket
+import tempfile
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dltb  # noqa: F401
+from dltb.comm import Comm, collective_time_us, parse_topology, recommend_bucket_mb, ring_factor
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = Comm()
+        assert (c.world, c.rank) == (world, rank)
+        n = 8
+        # all-reduce of a slice of a flat buffer, asynchronous, then wait_all
+        flat = torch.arange(3 * n, dtype=torch.float32) + 100 * rank
+        c.all_reduce(flat[n:2 * n])
+        assert c.pending == 1
+        c.wait_all()
+        ar = flat[n:2 * n].clone()
+        # reduce-scatter into this rank's chunk
+        inp = torch.arange(world * n, dtype=torch.float32) * (rank + 1)
+        out = torch.empty(n)
+        c.reduce_scatter(out, inp, async_op=False)
+        # in-place all-gather (this rank's slice of the output is the input)
+        full = torch.zeros(world * n)
+        full[rank * n:(rank + 1) * n] = rank + 1
+        w = c.all_gather(full, full[rank * n:(rank + 1) * n], track=False)
+        w.wait()
+        assert c.pending == 0
+        mx = c.max_scalar(float(rank), torch.device("cpu"))
+        torch.save({"ar": ar, "rs": out, "ag": full, "max": mx, "stats": dict(c.stats),
+                    "wire": c.wire_bytes()}, f"{out_path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_comm_world2():
+    world, n = 2, 8
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r")
+        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    base = torch.arange(n, 2 * n, dtype=torch.float32)
+    for r in range(world):
+        x = res[r]
+        assert torch.equal(x["ar"], 2 * base + 100)                      # (b) + (b + 100)
+        full_sum = torch.arange(world * n, dtype=torch.float32) * 3      # ranks scale by 1 and 2
+        assert torch.equal(x["rs"], full_sum[r * n:(r + 1) * n])
+        assert torch.equal(x["ag"], torch.tensor([1.0] * n + [2.0] * n))
+        assert x["max"] == 1.0
+        st = x["stats"]
+        assert st["all_reduce"]["calls"] == 1 and st["reduce_scatter"]["calls"] == 1
+        assert st["all_reduce"]["wire_bytes"] == int(n * 4 * ring_factor("all_reduce", 2))
+        assert st["reduce_scatter"]["wire_bytes"] == int(world * n * 4 * 0.5)
+        assert st["all_gather"]["wire_bytes"] == int(world * n * 4 * 0.5)
+        assert x["wire"] == sum(v["wire_bytes"] for v in st.values())
+
+
+def test_comm_single_process_is_noop():
+    c = Comm()
+    t = torch.ones(4)
+    assert c.all_reduce(t).wait() and torch.equal(t, torch.ones(4))
+    out = torch.empty(4)
+    c.reduce_scatter(out, torch.full((4,), 3.0))
+    assert torch.equal(out, torch.full((4,), 3.0))
+    full = torch.zeros(4)
+    c.all_gather(full, full)          # in place: nothing to move
+    assert c.pending == 0 and c.wire_bytes() == 0
+
+
+def test_topology_model():
+    assert ring_factor("all_reduce", 8) == 2 * 7 / 8 and ring_factor("all_gather", 1) == 0.0
+    # the recommended bucket is the smallest power of two whose fixed cost is <= 20 % of its transfer
+    alpha = collective_time_us("reduce_scatter", 0, 8)
+    for w in (2, 4, 8):
+        mb = recommend_bucket_mb(w)
+        xfer = collective_time_us("reduce_scatter", int(mb * (1 << 20)), w) - alpha
+        half = collective_time_us("reduce_scatter", int(mb * (1 << 19)), w) - alpha
+        assert alpha <= 0.2 * xfer and alpha > 0.2 * half
+    assert collective_time_us("all_reduce", 1 << 30, 1) == 0.0
+    txt = """============================ ROCm System Management Interface ============================
+================================ Link Type between two GPUs ================================
+       GPU0         GPU1         GPU2
+GPU0   0            XGMI         XGMI
+GPU1   XGMI         0            XGMI
+GPU2   XGMI         XGMI         0
+"""
+    links = parse_topology(txt)
+    assert links[(0, 1)] == "XGMI" and (0, 0) not in links and len(links) == 6

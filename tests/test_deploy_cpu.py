@@ -60,3 +60,16 @@ def test_collective_sweep_gloo(tmp_path):
     rows = json.loads(out.read_text())
     assert {x["op"] for x in rows} == {"all_reduce", "reduce_scatter", "all_gather"}
     assert all(x["busbw_GBps"] > 0 for x in rows)
+
+
+def test_verify_offline_local():
+    """scripts/verify_offline.sh (reference R38) in --local mode: imports, extension code object,
+    model instantiation with the expected parameter counts, dataset, one CPU step."""
+    import subprocess
+    from dltb.ops._ext import so_path
+    env = dict(os.environ, VERIFY_ALLOW_NO_EXT="0" if so_path() else "1")
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "verify_offline.sh"), "--local"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "OFFLINE VERIFICATION PASSED" in r.stdout
+    assert "TinyGPT tier A: 236.41M params" in r.stdout
