@@ -250,6 +250,9 @@ void embed_bwd(const Tensor& dx, const Tensor& idx, const optional<Tensor>& dwte
     check_contig_bf16(*dwte, "dwte");
     TORCH_CHECK(dwte->size(1) == d, "embed_bwd: dwte shape");
     auto flat = idx.reshape({-1}).contiguous();
+    if (dltb_embed_bwd_tok_scan(dx.data_ptr(), flat.data_ptr<int64_t>(), dwte->data_ptr(), (int)(B * T),
+                                (int)d, thr_of(p), scale_of(p), sp, site, cur_stream()))
+      return;
     auto sorted = at::sort(flat);
     auto ids = std::get<0>(sorted).contiguous();
     auto perm = std::get<1>(sorted).contiguous();
@@ -272,6 +275,42 @@ Tensor xent_fwd_bwd_(const Tensor& logits, const Tensor& targets, int64_t ignore
   dltb_xent_fwd_bwd(logits.data_ptr(), targets.data_ptr<int64_t>(), loss.data_ptr<float>(), (int)N,
                     (int)V, ignore_index, cur_stream());
   return loss;
+}
+
+// mean loss over non-ignored targets, device side: returns f32[2] = (mean, max(count, 1))
+Tensor xent_mean(const Tensor& loss_rows, const Tensor& targets, int64_t ignore_index) {
+  check_cuda(loss_rows, "loss_rows");
+  check_cuda(targets, "targets");
+  TORCH_CHECK(loss_rows.scalar_type() == at::kFloat && loss_rows.is_contiguous(), "xent_mean: loss f32");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous() &&
+              targets.numel() == loss_rows.numel(), "xent_mean: targets int64 [N]");
+  auto out = at::empty({2}, loss_rows.options());
+  dltb_xent_mean(loss_rows.data_ptr<float>(), targets.data_ptr<int64_t>(), (int)loss_rows.numel(),
+                 ignore_index, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
+// y = x * num[0] / den[0] (device scalars); optionally stores the scale into g_out[0]
+Tensor scale_by(const Tensor& x, const Tensor& num, const optional<Tensor>& den, const optional<Tensor>& g_out) {
+  check_contig_bf16(x, "x");
+  TORCH_CHECK(x.numel() % 8 == 0, "scale_by: numel % 8");
+  check_cuda(num, "num");
+  TORCH_CHECK(num.scalar_type() == at::kFloat && num.numel() >= 1, "scale_by: num f32");
+  const float* dp = nullptr;
+  if (den.has_value()) {
+    check_cuda(*den, "den");
+    TORCH_CHECK(den->scalar_type() == at::kFloat && den->numel() >= 1, "scale_by: den f32");
+    dp = den->data_ptr<float>();
+  }
+  float* gp = nullptr;
+  if (g_out.has_value()) {
+    check_cuda(*g_out, "g_out");
+    TORCH_CHECK(g_out->scalar_type() == at::kFloat && g_out->numel() >= 1, "scale_by: g_out f32");
+    gp = g_out->data_ptr<float>();
+  }
+  auto y = at::empty_like(x);
+  dltb_scale(x.data_ptr(), y.data_ptr(), x.numel(), num.data_ptr<float>(), dp, gp, cur_stream());
+  return y;
 }
 
 // ------------------------------------------------------------------------------ optimizer
@@ -586,7 +625,8 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K, bool tn, int64_t cfg) {
 }
 
 Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const optional<Tensor>& bias,
-            bool tn, bool accumulate, int64_t splits, int64_t cfg, int64_t pf, int64_t gm) {
+            bool tn, bool accumulate, int64_t splits, int64_t cfg, int64_t pf, int64_t gm,
+            const optional<Tensor>& alpha) {
   check_bf16(a, "a");
   check_bf16(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm: 2-D, inner dim contiguous");
@@ -613,11 +653,17 @@ Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const
     TORCH_CHECK(bias->numel() == N, "gemm: bias size");
     bp = bias->data_ptr();
   }
+  const float* ap = nullptr;
+  if (alpha.has_value()) {
+    check_cuda(*alpha, "alpha");
+    TORCH_CHECK(alpha->scalar_type() == at::kFloat && alpha->numel() >= 1, "gemm: alpha f32 device scalar");
+    ap = alpha->data_ptr<float>();
+  }
   Tensor part;
   if (splits > 1) part = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
   dltb_gemm(a.data_ptr(), b.data_ptr(), c.data_ptr(), bp, splits > 1 ? part.data_ptr<float>() : nullptr,
             a.stride(0), b.stride(0), c.stride(0), (int)M, (int)N, (int)K, tn, accumulate ? 1 : 0,
-            (int)splits, (int)cfg, (int)pf, (int)gm, cur_stream());
+            (int)splits, (int)cfg, (int)pf, (int)gm, ap, cur_stream());
   return c;
 }
 
@@ -651,8 +697,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
   m.def("colpart", &colpart);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias"), py::arg("tn"),
-        py::arg("accumulate"), py::arg("splits") = 1, py::arg("cfg") = 0, py::arg("pf") = 0, py::arg("gm") = 1);
+        py::arg("accumulate"), py::arg("splits") = 1, py::arg("cfg") = 0, py::arg("pf") = 0, py::arg("gm") = 1,
+        py::arg("alpha") = py::none());
   m.def("gemm_supported", &gemm_supported);
+  m.def("xent_mean", &xent_mean);
+  m.def("scale_by", &scale_by, py::arg("x"), py::arg("num"), py::arg("den") = py::none(),
+        py::arg("g_out") = py::none());
   m.def("transpose_into", &transpose_into);
   m.def("colreduce_multi", &colreduce_multi);
   m.def("arch", []() { return std::string("gfx950"); });

@@ -283,7 +283,33 @@ __global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict
   }
 }
 
+// y = x * (num[0] / den[0]) with the scale read on the device (no host sync); block 0 thread 0
+// also stores the scale to g_out (re-used by the next kernel, e.g. as a GEMM alpha).
+__global__ __launch_bounds__(256) void scale_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                   long n8, const float* __restrict__ num,
+                                                   const float* __restrict__ den, float* __restrict__ g_out) {
+  const float s = num[0] / (den ? den[0] : 1.f);
+  if (g_out && blockIdx.x == 0 && threadIdx.x == 0) g_out[0] = s;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    float f[8];
+    unpack8(ld16<uint4>(x + i * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] *= s;
+    *reinterpret_cast<uint4*>(y + i * 8) = pack8(f);
+  }
+}
+
 }  // namespace
+
+void dltb_scale(const void* x, void* y, long n, const float* num, const float* den, float* g_out,
+                hipStream_t st) {
+  const long n8 = n / 8;
+  long grid = (n8 + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, st, (const bf16_t*)x, (bf16_t*)y, n8, num,
+                     den, g_out);
+}
 
 // ---------------------------------------------------------------------------------------- API
 void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st) {

@@ -29,6 +29,7 @@ struct GemmArgs {
   const bf16_t* b;
   bf16_t* c;
   const bf16_t* bias;
+  const float* alpha;   // optional device scalar multiplying A B (before bias / accumulate)
   float* part;          // split-K partials [splits][M][N] (fp32), null without split-K
   long lda, ldb, ldc;
   int M, N, K;
@@ -154,6 +155,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   }
 
   // ---- epilogue: lane -> row m, register group q -> columns n .. n+3
+  const float al = (g.alpha && splits == 1) ? *g.alpha : 1.f;
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = m0 + wm * WM + 32 * i + r;
@@ -162,7 +164,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = n0 + wn * WN + 32 * j + 8 * q + 4 * h;
-        float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        float v[4] = {acc[i][j][4 * q] * al, acc[i][j][4 * q + 1] * al, acc[i][j][4 * q + 2] * al,
+                      acc[i][j][4 * q + 3] * al};
         if (splits > 1) {
           *reinterpret_cast<float4*>(g.part + ((size_t)split * g.M + m) * g.N + n) = make_float4(v[0], v[1], v[2], v[3]);
           continue;
@@ -188,6 +191,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 // split-K reduction: C = sum_s part[s] (+ bias) (+ C)
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int splits) {
   const long total4 = (long)g.M * g.N / 4;
+  const float al = g.alpha ? *g.alpha : 1.f;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
     const long e = i * 4;
     const int m = (int)(e / g.N), n = (int)(e % g.N);
@@ -196,7 +200,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int splits
       const float4 t = *reinterpret_cast<const float4*>(g.part + (size_t)k * g.M * g.N + e);
       s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     }
-    float v[4] = {s.x, s.y, s.z, s.w};
+    float v[4] = {s.x * al, s.y * al, s.z * al, s.w * al};
     if (g.bias) {
       const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
       v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
@@ -253,8 +257,9 @@ bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg) {
 
 int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
               long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
-              hipStream_t st) {
+              const float* alpha, hipStream_t st) {
   GemmArgs g{};
+  g.alpha = alpha;
   g.pf = pf;
   g.gm = gm;
   g.a = (const bf16_t*)a;

@@ -43,6 +43,9 @@ void dltb_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* 
 void dltb_embed_bwd_pos(const void* dx, void* dwpe, int B, int T, int P, int d, int accumulate,
                         uint32_t thr16, float scale, const int64_t* seed, int64_t site,
                         hipStream_t st);
+bool dltb_embed_bwd_tok_scan(const void* dx, const int64_t* ids, void* dwte, int N, int d,
+                             uint32_t thr16, float scale, const int64_t* seed, int64_t site,
+                             hipStream_t st);
 void dltb_embed_bwd_tok(const void* dx, const int64_t* sorted_ids, const int64_t* perm,
                         void* dwte, int N, int d, uint32_t thr16, float scale,
                         const int64_t* seed, int64_t site, hipStream_t st);
@@ -109,4 +112,12 @@ void dltb_colreduce_multi(const DltbColRedSeg* segs, int nseg, hipStream_t st);
 // ---- gemm.hip: C[M,N] = A B (+bias) (+C); NT: A [M][K], B [N][K]; TN: A [K][M], B [K][N]
 bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg);
 int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
-              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm, hipStream_t st);
+              long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
+              const float* alpha, hipStream_t st);
+
+// device-scalar helpers (head backward: no host sync)
+void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,
+                    hipStream_t st);
+void dltb_scale(const void* x, void* y, long n, const float* num, const float* den, float* g_out,
+                hipStream_t st);
+

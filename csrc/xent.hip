@@ -69,7 +69,32 @@ __global__ __launch_bounds__(512) void xent_kernel(bf16_t* __restrict__ logits,
   }
 }
 
+// mean over non-ignored rows in one 1024-thread workgroup (fixed summation order):
+//   out[0] = sum(loss) / max(count, 1),  out[1] = max(count, 1)
+__global__ __launch_bounds__(1024) void xent_mean_kernel(const float* __restrict__ loss,
+                                                        const int64_t* __restrict__ targets, int N,
+                                                        int64_t ignore_index, float* __restrict__ out) {
+  __shared__ float red[16];
+  float s = 0.f, c = 0.f;
+  for (int i = threadIdx.x; i < N; i += 1024) {
+    s += loss[i];
+    c += targets[i] != ignore_index ? 1.f : 0.f;
+  }
+  s = block_sum(s, red);
+  c = block_sum(c, red);
+  if (threadIdx.x == 0) {
+    c = fmaxf(c, 1.f);
+    out[0] = s / c;
+    out[1] = c;
+  }
+}
+
 }  // namespace
+
+void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,
+                    hipStream_t st) {
+  hipLaunchKernelGGL(xent_mean_kernel, dim3(1), dim3(1024), 0, st, loss, targets, N, ignore_index, out);
+}
 
 void dltb_xent_fwd_bwd(void* logits, const int64_t* targets, float* loss, int N, int V,
                        int64_t ignore_index, hipStream_t st) {

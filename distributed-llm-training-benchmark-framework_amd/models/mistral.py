@@ -168,8 +168,8 @@ class _HeadFn(torch.autograd.Function):
         kept = logits.clone() if return_logits else None
         tg = targets.reshape(-1)
         loss_rows = F_.xent_fwd_bwd_(logits, tg, -1)
-        count = (tg != -1).sum().clamp(min=1).to(torch.float32)
-        loss = loss_rows.sum() / count
+        lc = F_.xent_mean(loss_rows, tg, -1)          # (mean, count) on the device
+        loss, count = lc[0], lc[1:2]
         rt.release_forward(unit)
         ctx.model, ctx.no_loss = model, False
         ctx.saved = (x, h, rstd, logits, count)
@@ -186,10 +186,10 @@ class _HeadFn(torch.autograd.Function):
         (x, h, rstd, dl, count) = ctx.saved
         ctx.saved = None
         w_norm, w_head = rt.acquire_backward(unit)
-        g = dloss.to(torch.float32) / count
         dwh, acc_h = rt.grad_slot(unit, 1)
-        F_.linear_wgrad(dl, (h * g).to(h.dtype), dwh, None, acc_h)
-        dh = (torch.mm(dl, w_head) * g).to(h.dtype)
+        hs, g = F_.scale_by(h, dloss, count)                      # g = dloss / count (device)
+        F_.linear_wgrad(dl, hs, dwh, None, acc_h)
+        dh = F_.head_dgrad(dl, w_head, rt.weight_t(unit, 1, w_head), g)
         gw, acc = rt.grad_slot(unit, 0)
         dx = F_.norm_bwd(dh, x, w_norm, None, rstd, None, gw, None, acc, True)
         rt.grads_ready(unit)

@@ -180,8 +180,8 @@ class _HeadFn(torch.autograd.Function):
         kept = logits.clone() if return_logits else None
         tg = targets.reshape(-1)
         loss_rows = F_.xent_fwd_bwd_(logits, tg, -1)
-        count = (tg != -1).sum().clamp(min=1).to(torch.float32)
-        loss = loss_rows.sum() / count
+        lc = F_.xent_mean(loss_rows, tg, -1)          # (mean, count) on the device
+        loss, count = lc[0], lc[1:2]
         rt.release_forward(model.unit_head)
         ctx.model, ctx.no_loss = model, False
         ctx.saved = (x, h, mean, rstd, logits, count)
@@ -199,12 +199,11 @@ class _HeadFn(torch.autograd.Function):
         ctx.saved = None
         lnw, lnb = rt.acquire_backward(model.unit_head)
         wte = rt.acquire_tied(model.unit_embed)[0]
-        g = (dloss.to(torch.float32) / count)
         par = GradStreams(x.device)
         dw, acc_w = rt.grad_slot(model.unit_embed, 0)            # tied lm_head / wte
-        hs = (h * g).to(h.dtype)
+        hs, g = F_.scale_by(h, dloss, count)                      # g = dloss / count (device)
         F_.linear_wgrad(dl, hs, dw, None, acc_w, par)              # side stream, overlaps dh
-        dh = (torch.mm(dl, wte) * g).to(h.dtype)
+        dh = F_.head_dgrad(dl, wte, rt.weight_t(model.unit_embed, 0, wte), g)
         gw, acc = rt.grad_slot(model.unit_head, 0)
         gb, _ = rt.grad_slot(model.unit_head, 1)
         dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False, par)

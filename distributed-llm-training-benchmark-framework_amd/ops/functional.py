@@ -174,6 +174,38 @@ def xent_fwd_bwd_(logits2d, targets1d, ignore_index=-1):
     return ref.xent_fwd_bwd_(logits2d, targets1d, ignore_index)
 
 
+def xent_mean(loss_rows, targets1d, ignore_index=-1):
+    """f32[2] = (mean loss over non-ignored rows, max(count, 1)), computed on the device (one
+    launch on MI355X instead of compare / sum / clamp / cast / div)."""
+    if _gpu(loss_rows):
+        return ext().xent_mean(loss_rows, targets1d, ignore_index)
+    count = (targets1d != ignore_index).sum().clamp(min=1).to(torch.float32)
+    return torch.stack([loss_rows.sum() / count, count])
+
+
+def scale_by(x, num, den=None):
+    """(x * num/den, g = num/den as f32[1]) with the scale kept on the device (no host sync)."""
+    num = num.to(torch.float32).reshape(-1)
+    if _gpu(x):
+        g = torch.empty(1, device=x.device, dtype=torch.float32)
+        return ext().scale_by(x.contiguous(), num, den, g), g
+    g = num[:1] / den.reshape(-1)[:1] if den is not None else num[:1].clone()
+    return (x * g).to(x.dtype), g
+
+
+def head_dgrad(dl, w, wt, g):
+    """dX = g * dL W for an LM head with weight W [V, d].  On MI355X with a cached W^T this is the
+    split-K MFMA GEMM (NT form, g applied as a device alpha in the split-K reduction): K = V is
+    long and the output (tokens x d) small, which hipBLASLt's NN kernels handle poorly."""
+    if _gpu(dl) and wt is not None and dl.stride(1) == 1:
+        M, K = dl.shape
+        N = wt.shape[0]
+        C = ext()
+        if C.gemm_supported(M, N, K, False, 2):
+            return C.gemm(dl, wt, None, None, False, False, 4, 2, 0, 1, g)
+    return (torch.mm(dl, w) * g).to(dl.dtype)
+
+
 # ------------------------------------------------------------------------------ attention
 def attn_mask(B, T, Hq, p, seed, site, like, par=None):
     """Packed dropout keep-bits for attention (GPU only; launched on the side stream so it overlaps
