@@ -76,7 +76,7 @@ def main():
             from dltb.ops._ext import ext
             C = ext()
             for cfg in range(6):
-                for sp in (1, 2):
+                for sp in ((1, 2, 4, 8) if max(N, K, M) >= 8192 else (1, 2)):
                     for pf in ((0, 2, 4, 8) if sp == 1 else (0,)):
                         for gm in ((1, 2, 4, 8) if sp == 1 else (1,)):
                             tag = f"c{cfg}s{sp}p{pf}g{gm}"

@@ -73,3 +73,31 @@ def test_verify_offline_local():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "OFFLINE VERIFICATION PASSED" in r.stdout
     assert "TinyGPT tier A: 236.41M params" in r.stdout
+
+
+def _fake_kubectl(tmp_path, plugin_pods):
+    """A kubectl stand-in for scripts/check_cluster_gpus.sh (no cluster in the test container)."""
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    k = bindir / "kubectl"
+    k.write_text(f"""#!/usr/bin/env bash
+case "$*" in
+  "cluster-info") echo ok ;;
+  "config current-context") echo test-ctx ;;
+  *"-l name=amdgpu-dp-ds"*) for i in $(seq 1 {plugin_pods}); do echo pod/amdgpu-dp-ds-$i; done ;;
+  "get pods -A -o name") echo pod/coredns ;;
+  "describe nodes") printf 'Name: mi355x-0\\n  amd.com/gpu: 8\\n' ;;
+  *) exit 0 ;;
+esac
+""")
+    k.chmod(0o755)
+    return dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}")
+
+
+@pytest.mark.parametrize("plugin_pods,ok", [(2, True), (0, False)])
+def test_check_cluster_gpus(tmp_path, plugin_pods, ok):
+    env = _fake_kubectl(tmp_path, plugin_pods)
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "check_cluster_gpus.sh")], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert (r.returncode == 0) == ok, r.stdout + r.stderr
+    assert ("CLUSTER READY" in r.stdout) == ok
