@@ -49,6 +49,7 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
   const int seg = blk_seg[blockIdx.x];
   const int64_t start = blk_start[blockIdx.x];
   const int64_t seg_end = seg_ostart[seg] + seg_len[seg];
+  DLTB_DCHECK(seg >= 0 && start >= seg_ostart[seg] && start < seg_end);
   bf16_t* dst = reinterpret_cast<bf16_t*>(seg_dst[seg]);
   const int64_t dst_base = start - seg_ostart[seg];
   const float gs = gscale ? *gscale : 1.f;

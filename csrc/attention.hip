@@ -211,6 +211,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   const int b = bh / P.Hq, hq = bh % P.Hq, hk = hq / (P.Hq / P.Hkv);
   const int q0 = qb * kBlockRows + qw * 32;
   const int qi = q0 + r;
+  DLTB_DCHECK(qi < T && bh < P.B * P.Hq && hk < P.Hkv);
 
   bfx8 qf[D / 16];
   {

@@ -9,6 +9,13 @@ headers, and everything is linked into
 so the built ``.so`` travels with the repository snapshot to the GPU box.
 
 Usage:  python csrc/build.py [--force] [--debug] [-j N]
+
+``--debug`` builds a separate checked extension (``build/debug/_C.<EXT_SUFFIX>``, objects under
+``build/csrc-debug``; the release ``.so`` is untouched): kernels at -O1 -g with ``DLTB_DEBUG=1``,
+which turns on the device-side bound checks of ``common.h`` (``DLTB_DCHECK``: printf of the
+failing condition, kernel name and block, then ``s_trap``), and host code with
+``-D_GLIBCXX_ASSERTIONS``.  Load it with ``DLTB_EXT_PATH=build/debug/_C...so``.  (GPU
+AddressSanitizer needs xnack+ code objects, which the target pool does not run.)
 """
 import argparse
 import concurrent.futures as cf
@@ -27,8 +34,9 @@ ARCH = os.environ.get("DLTB_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
-def ext_path() -> str:
-    return os.path.join(PKG_DIR, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+def ext_path(debug: bool = False) -> str:
+    name = "_C" + sysconfig.get_config_var("EXT_SUFFIX")
+    return os.path.join(ROOT, "build", "debug", name) if debug else os.path.join(PKG_DIR, name)
 
 
 def _headers():
@@ -72,26 +80,29 @@ def _torch_flags():
 def build(force: bool = False, debug: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
     cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
-    os.makedirs(BUILD_DIR, exist_ok=True)
+    bdir = BUILD_DIR + ("-debug" if debug else "")
+    os.makedirs(bdir, exist_ok=True)
     hdrs = _headers()
-    opt = ["-O0", "-g", "-DDLTB_DEBUG=1"] if debug else ["-O3"]
+    opt = ["-O1", "-g", "-DDLTB_DEBUG=1"] if debug else ["-O3"]
     hip_srcs = sorted(glob.glob(os.path.join(HERE, "*.hip")))
     jobs_list = []
     objs = []
     for src in hip_srcs:
-        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _stale(obj, src, hdrs):
             jobs_list.append([hipcc, "-c", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", *opt,
                               "-munsafe-fp-atomics", "-I", HERE, src, "-o", obj])
     incs, tflags, libdir = _torch_flags()
     bsrc = os.path.join(HERE, "bindings.cpp")
-    bobj = os.path.join(BUILD_DIR, "bindings.cpp.o")
+    bobj = os.path.join(bdir, "bindings.cpp.o")
     objs.append(bobj)
+    hopt = ["-O1", "-g", "-D_GLIBCXX_ASSERTIONS", "-DDLTB_DEBUG=1"] if debug else ["-O2"]
     if force or _stale(bobj, bsrc, hdrs):
-        jobs_list.append([cxx, "-c", "-fPIC", "-std=c++17", "-O2", *tflags,
+        jobs_list.append([cxx, "-c", "-fPIC", "-std=c++17", *hopt, *tflags,
                           *[f"-I{p}" for p in incs], "-I", HERE, bsrc, "-o", bobj])
-    out = ext_path()
+    out = ext_path(debug)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     if jobs_list:
         if verbose:
             print(f"[dltb.build] compiling {len(jobs_list)} translation unit(s) for {ARCH}", flush=True)

@@ -40,6 +40,7 @@ __global__ __launch_bounds__(256) void colpart_kernel(ColPartArgs A) {
   const int r0 = blockIdx.y * rps;
   const int r1 = min(S.N, r0 + rps);
   const int kind = S.kind;
+  DLTB_DCHECK(k % 8 == 0 && kind >= 0 && kind <= 4 && r1 <= S.N);
   float a0[8], a1[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { a0[e] = 0.f; a1[e] = 0.f; }

@@ -10,6 +10,23 @@
 
 #define DLTB_DEV __device__ __forceinline__
 
+// Device-side bound checks of the checked build (csrc/build.py --debug => DLTB_DEBUG=1): print the
+// failing condition with the kernel and block, then trap.  Compiled out of release builds.
+#if defined(DLTB_DEBUG) && DLTB_DEBUG
+#define DLTB_DCHECK(cond)                                                                        \
+  do {                                                                                           \
+    if (!(cond)) {                                                                               \
+      printf("[dltb DCHECK] %s failed in %s (block %d,%d thread %d)\n", #cond, __func__,         \
+             (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);                                \
+      __builtin_trap();                                                                          \
+    }                                                                                            \
+  } while (0)
+#else
+#define DLTB_DCHECK(cond) \
+  do {                    \
+  } while (0)
+#endif
+
 typedef uint16_t bf16_t;                                     // raw bf16 bits
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(256) void embed_bwd_tok_scan_kernel(
   if (i >= N) return;
   const long id = ids[i];
   if (id < 0) return;
+  DLTB_DCHECK(d % 8 == 0 && d <= kScanMaxChunks * 512);
   for (int base = 0; base < i; base += 64) {            // an earlier duplicate owns this id
     const int j = base + lane;
     if (__ballot(j < i && ids[j] == id)) return;

@@ -75,6 +75,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   const int m0 = mb * BM, n0 = nb * BN;
   const int kbeg = split * g.ksplit;
   const int nk = min(g.ksplit, g.K - kbeg) / kBK;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && kbeg + nk * kBK <= g.K && nk > 0);
 
   // L2 prefetch of k-step kt + pf: one 4-byte LDS-DMA per 128-byte line of the stage (BM + BN lines),
   // landing in a scratch LDS slot.  The XCD's L2 then already holds the lines when the real stage is

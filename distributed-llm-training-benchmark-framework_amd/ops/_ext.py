@@ -2,7 +2,8 @@
 
 GPU code paths call :func:`ext` which raises loudly when the extension is missing — there is no
 silent eager fallback on the GPU.  The torch reference implementations in :mod:`dltb.ops.ref`
-serve CPU tests only.
+serve CPU tests only.  ``DLTB_EXT_PATH`` loads another build of the same module instead (the
+checked ``csrc/build.py --debug`` extension).
 """
 import importlib
 import os
@@ -17,7 +18,17 @@ def _try_load():
         return
     try:
         import torch  # noqa: F401  (libtorch must be loaded before the extension)
-        _C = importlib.import_module(__package__.rsplit(".", 1)[0] + "._C")
+        name = __package__.rsplit(".", 1)[0] + "._C"
+        alt = os.environ.get("DLTB_EXT_PATH")
+        if alt:
+            import importlib.util
+            import sys
+            spec = importlib.util.spec_from_file_location(name, alt)
+            _C = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_C)
+            sys.modules[name] = _C
+        else:
+            _C = importlib.import_module(name)
     except Exception as e:  # pragma: no cover - depends on the build
         _ERR = e
 

@@ -101,3 +101,22 @@ def test_check_cluster_gpus(tmp_path, plugin_pods, ok):
                        capture_output=True, text=True, timeout=60)
     assert (r.returncode == 0) == ok, r.stdout + r.stderr
     assert ("CLUSTER READY" in r.stdout) == ok
+
+
+def test_debug_extension_is_separate_and_loadable():
+    """csrc/build.py --debug writes build/debug/_C*.so (never the release module) and DLTB_EXT_PATH
+    loads it in place of the in-tree extension."""
+    sys.path.insert(0, os.path.join(ROOT, "csrc"))
+    try:
+        import build as b
+    finally:
+        sys.path.pop(0)
+    assert b.ext_path(True) != b.ext_path(False)
+    assert os.path.dirname(b.ext_path(False)).endswith("distributed-llm-training-benchmark-framework_amd")
+    dbg = b.ext_path(True)
+    if not os.path.exists(dbg):
+        pytest.skip("checked extension not built here (python csrc/build.py --debug)")
+    r = subprocess.run([sys.executable, "-c", "import dltb; from dltb.ops._ext import so_path; print(so_path())"],
+                       cwd=ROOT, env=dict(os.environ, DLTB_EXT_PATH=dbg), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith(os.path.relpath(dbg, ROOT).split(os.sep, 1)[1]) or dbg in r.stdout
