@@ -6,7 +6,9 @@ serve CPU tests only.  ``DLTB_EXT_PATH`` loads another build of the same module 
 checked ``csrc/build.py --debug`` extension).
 """
 import importlib
+import importlib.util
 import os
+import sys
 
 _C = None
 _ERR = None
@@ -21,8 +23,6 @@ def _try_load():
         name = __package__.rsplit(".", 1)[0] + "._C"
         alt = os.environ.get("DLTB_EXT_PATH")
         if alt:
-            import importlib.util
-            import sys
             spec = importlib.util.spec_from_file_location(name, alt)
             _C = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(_C)
