@@ -499,6 +499,31 @@ Tensor norm_bwd_dx(const Tensor& dy, const Tensor& s, const Tensor& w, const opt
   return dx;
 }
 
+// fused norm backward: (dx, part[K, P, d] f32) with K = (rms ? 1 : 2) + dx_sum; see norm.hip
+std::tuple<Tensor, Tensor> norm_bwd_fused(const Tensor& dy, const Tensor& s, const Tensor& w,
+                                          const optional<Tensor>& mean, const Tensor& rstd,
+                                          const optional<Tensor>& dres, bool rms, bool dx_sum) {
+  check_contig_bf16(dy, "dy");
+  check_contig_bf16(s, "s");
+  check_contig_bf16(w, "w");
+  const int64_t d = dy.size(-1);
+  const int64_t N = dy.numel() / d;
+  TORCH_CHECK(dltb_norm_bwd_fused_supported((int)d), "norm_bwd_fused: unsupported width");
+  TORCH_CHECK(s.sizes() == dy.sizes() && w.numel() == d, "norm_bwd_fused shapes");
+  TORCH_CHECK(rstd.numel() == N && (rms || (mean.has_value() && mean->numel() == N)), "norm stats");
+  if (dres.has_value()) {
+    check_contig_bf16(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == dy.sizes(), "norm_bwd_fused: dres shape");
+  }
+  auto dx = at::empty_like(dy);
+  const int64_t K = (rms ? 1 : 2) + (dx_sum ? 1 : 0);
+  auto part = at::empty({K, (int64_t)dltb_norm_bwd_fused_blocks((int)N), d}, dy.options().dtype(at::kFloat));
+  dltb_norm_bwd_fused(dy.data_ptr(), s.data_ptr(), w.data_ptr(), rms ? nullptr : mean->data_ptr<float>(),
+                      rstd.data_ptr<float>(), dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(),
+                      part.data_ptr<float>(), (int)N, (int)d, rms, dx_sum, cur_stream());
+  return {dx, part};
+}
+
 void norm_bwd_dgamma(const Tensor& dy, const Tensor& s, const optional<Tensor>& mean, const Tensor& rstd,
                      const Tensor& gw, const optional<Tensor>& gb, bool accumulate, bool rms) {
   check_contig_bf16(dy, "dy");
@@ -626,7 +651,7 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K, bool tn, int64_t cfg) {
 
 Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const optional<Tensor>& bias,
             bool tn, bool accumulate, int64_t splits, int64_t cfg, int64_t pf, int64_t gm,
-            const optional<Tensor>& alpha) {
+            const optional<Tensor>& alpha, int64_t stages) {
   check_bf16(a, "a");
   check_bf16(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1, "gemm: 2-D, inner dim contiguous");
@@ -663,7 +688,7 @@ Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const
   if (splits > 1) part = at::empty({splits, M, N}, a.options().dtype(at::kFloat));
   dltb_gemm(a.data_ptr(), b.data_ptr(), c.data_ptr(), bp, splits > 1 ? part.data_ptr<float>() : nullptr,
             a.stride(0), b.stride(0), c.stride(0), (int)M, (int)N, (int)K, tn, accumulate ? 1 : 0,
-            (int)splits, (int)cfg, (int)pf, (int)gm, ap, cur_stream());
+            (int)splits, (int)cfg, (int)pf, (int)gm, ap, cur_stream(), (int)stages);
   return c;
 }
 
@@ -695,10 +720,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
+  m.def("norm_bwd_fused", &norm_bwd_fused);
+  m.def("norm_bwd_fused_supported", [](int64_t d) { return dltb_norm_bwd_fused_supported((int)d); });
   m.def("colpart", &colpart);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias"), py::arg("tn"),
         py::arg("accumulate"), py::arg("splits") = 1, py::arg("cfg") = 0, py::arg("pf") = 0, py::arg("gm") = 1,
-        py::arg("alpha") = py::none());
+        py::arg("alpha") = py::none(), py::arg("stages") = 0);
   m.def("gemm_supported", &gemm_supported);
   m.def("xent_mean", &xent_mean);
   m.def("scale_by", &scale_by, py::arg("x"), py::arg("num"), py::arg("den") = py::none(),

@@ -48,8 +48,11 @@ struct Geo {
   static constexpr int STAGE = A_BYTES + B_BYTES;
 };
 
+// NSTAGE >= 3: one workgroup per CU (a deep LDS-DMA ring, counted vmcnt across the barrier);
+// NSTAGE == 2: a double buffer small enough for two workgroups per CU (one wave of each per SIMD:
+// one wave's MFMAs cover the other's LDS reads and barrier waits).
 template <int BM, int BN, bool TN, int NSTAGE, bool PF>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, NSTAGE == 2 ? 2 : 1) void gemm_kernel(GemmArgs g) {
   using G = Geo<BM, BN, TN>;
   constexpr int WM = BM / 2, WN = BN / 2;          // wave tile
   constexpr int FM = WM / 32, FN = WN / 32;        // 32x32 MFMA tiles per wave
@@ -218,9 +221,8 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemmArgs g, int splits
   }
 }
 
-template <int BM, int BN, bool TN, bool PF>
-void launch_pf(const GemmArgs& g, int splits, hipStream_t st) {
-  constexpr int NSTAGE = Geo<BM, BN, TN>::STAGE <= 32768 ? 4 : 3;   // <= 128 KiB of LDS ring
+template <int BM, int BN, bool TN, bool PF, int NSTAGE>
+void launch_ns(const GemmArgs& g, int splits, hipStream_t st) {
   constexpr int smem = NSTAGE * Geo<BM, BN, TN>::STAGE + (PF ? 1024 : 0);
   static bool attr = false;
   if (!attr) {
@@ -232,10 +234,19 @@ void launch_pf(const GemmArgs& g, int splits, hipStream_t st) {
   hipLaunchKernelGGL((gemm_kernel<BM, BN, TN, NSTAGE, PF>), dim3(tiles * splits), dim3(256), smem, st, g);
 }
 
+// stages == 2: double buffer (two or more workgroups per CU); otherwise the deep ring (<= 128 KiB,
+// one workgroup per CU)
+template <int BM, int BN, bool TN, bool PF>
+void launch_pf(const GemmArgs& g, int splits, int stages, hipStream_t st) {
+  constexpr int DEEP = Geo<BM, BN, TN>::STAGE <= 32768 ? 4 : 3;
+  if (stages == 2) launch_ns<BM, BN, TN, PF, 2>(g, splits, st);
+  else launch_ns<BM, BN, TN, PF, DEEP>(g, splits, st);
+}
+
 template <int BM, int BN, bool TN>
-void launch_t(const GemmArgs& g, int splits, hipStream_t st) {
-  if (g.pf > 0) launch_pf<BM, BN, TN, true>(g, splits, st);
-  else launch_pf<BM, BN, TN, false>(g, splits, st);
+void launch_t(const GemmArgs& g, int splits, int stages, hipStream_t st) {
+  if (g.pf > 0) launch_pf<BM, BN, TN, true>(g, splits, stages, st);
+  else launch_pf<BM, BN, TN, false>(g, splits, stages, st);
 }
 
 }  // namespace
@@ -258,7 +269,7 @@ bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg) {
 
 int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
               long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
-              const float* alpha, hipStream_t st) {
+              const float* alpha, hipStream_t st, int stages) {
   GemmArgs g{};
   g.alpha = alpha;
   g.pf = pf;
@@ -283,12 +294,12 @@ int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* pa
   if (splits > 1 && !part) return -1;
 #define DLTB_G(BM, BN)                                              \
   do {                                                              \
-    if (tn) launch_t<BM, BN, true>(g, splits, st);                  \
-    else launch_t<BM, BN, false>(g, splits, st);                    \
+    if (tn) launch_t<BM, BN, true>(g, splits, stages, st);          \
+    else launch_t<BM, BN, false>(g, splits, stages, st);            \
   } while (0)
   switch (cfg) {
-    case 1: launch_t<256, 128, false>(g, splits, st); break;
-    case 2: launch_t<128, 256, false>(g, splits, st); break;
+    case 1: launch_t<256, 128, false>(g, splits, stages, st); break;
+    case 2: launch_t<128, 256, false>(g, splits, stages, st); break;
     case 3: DLTB_G(128, 64); break;
     case 4: DLTB_G(64, 128); break;
     case 5: DLTB_G(64, 64); break;

@@ -19,6 +19,12 @@ void dltb_norm_bwd_dgamma(const void* dy, const void* s, const float* mean, cons
 void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,
                    const float* rstd, const void* dres, void* dx, float* part, void* gw, void* gb,
                    int accumulate, int N, int d, bool rms, hipStream_t st);
+// fused dx + column partials; part: [(rms ? 1 : 2) + dxsum][blocks(N)][d] fp32
+bool dltb_norm_bwd_fused_supported(int d);
+int dltb_norm_bwd_fused_blocks(int N);
+bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
+                         const float* rstd, const void* dres, void* dx, float* part, int N, int d,
+                         bool rms, bool dxsum, hipStream_t st);
 
 // elementwise.hip
 void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st);
@@ -113,7 +119,7 @@ void dltb_colreduce_multi(const DltbColRedSeg* segs, int nseg, hipStream_t st);
 bool dltb_gemm_supported(int M, int N, int K, bool tn, int cfg);
 int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* part, long lda, long ldb,
               long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
-              const float* alpha, hipStream_t st);
+              const float* alpha, hipStream_t st, int stages = 0);
 
 // device-scalar helpers (head backward: no host sync)
 void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,

@@ -160,6 +160,108 @@ __global__ __launch_bounds__(256) void norm_bwd_dx_kernel(
   }
 }
 
+// Fused backward, one pass over dy / s: dx (+ the residual gradient) AND the fp32 column partials of
+// dgamma = sum_r dy * xhat, dbeta = sum_r dy (LayerNorm only) and, with DXSUM, of the stored dx
+// itself (the bias gradient of the linear whose output entered this residual stream).  Each wave
+// owns `rpw` consecutive rows (one at TinyGPT's 2048 tokens) and keeps its column sums in registers;
+// the 8 waves fold through one [8][d] LDS image, one partial at a time.  part: [K][gridDim.x][d]
+// with K = (RMS ? 1 : 2) + DXSUM, summed into the gradient slots by colreduce_multi.  Replaces
+// norm_bwd_dx + a colpart launch.
+constexpr int kFusedWaves = 8;     // 512-thread blocks: two waves per SIMD at one block per CU
+
+template <int NV, bool RMS, bool HAS_RES_GRAD, bool DXSUM>
+__global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N, int d,
+    int rpw) {
+  extern __shared__ __attribute__((aligned(16))) float fold[];   // [kFusedWaves][d]
+  constexpr int K = (RMS ? 1 : 2) + (DXSUM ? 1 : 0);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nvec = d >> 3;
+  float wv[NV][8], acc[K][NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int idx = j * 64 + lane;
+    if (idx < nvec) unpack8(ld16<uint4>(w + idx * 8), wv[j]);
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[k][j][e] = 0.f;
+  }
+  const int r0 = (blockIdx.x * kFusedWaves + wid) * rpw;
+  const int r1 = min(N, r0 + rpw);
+  for (int row = r0; row < r1; ++row) {                  // wave-uniform trip count
+    const size_t base = (size_t)row * d;
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float g[NV][8], xh[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int idx = j * 64 + lane;
+      if (idx < nvec) {
+        float dyv[8], xv[8];
+        unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
+        unpack8(ld16<uint4>(s + base + idx * 8), xv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xh[j][e] = (xv[e] - mean) * rstd;
+          g[j][e] = dyv[e] * wv[j][e];
+          s1 += g[j][e];
+          s2 += g[j][e] * xh[j][e];
+          acc[0][j][e] += dyv[e] * xh[j][e];
+          if (!RMS) acc[1][j][e] += dyv[e];
+        }
+      }
+    }
+    s1 = RMS ? 0.f : wave_sum(s1) / (float)d;
+    s2 = wave_sum(s2) / (float)d;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int idx = j * 64 + lane;
+      if (idx < nvec) {
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = rstd * (g[j][e] - s1 - xh[j][e] * s2);
+        if (HAS_RES_GRAD) {
+          float rv[8];
+          unpack8(ld16<uint4>(dres + base + idx * 8), rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] += rv[e];
+        }
+        const uint4 ov = pack8(o);
+        *reinterpret_cast<uint4*>(dx + base + idx * 8) = ov;
+        if (DXSUM) {
+          unpack8(ov, o);                                // sum the rounded dx the next GEMM reads
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[K - 1][j][e] += o[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (k) __syncthreads();                              // the previous partial has been read
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int idx = j * 64 + lane;
+      if (idx < nvec) {
+        float4* f = reinterpret_cast<float4*>(fold + wid * d + idx * 8);
+        f[0] = make_float4(acc[k][j][0], acc[k][j][1], acc[k][j][2], acc[k][j][3]);
+        f[1] = make_float4(acc[k][j][4], acc[k][j][5], acc[k][j][6], acc[k][j][7]);
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += kFusedWaves * 64) {
+      float t = 0.f;
+#pragma unroll
+      for (int v = 0; v < kFusedWaves; ++v) t += fold[v * d + c];
+      part[((size_t)k * gridDim.x + blockIdx.x) * d + c] = t;
+    }
+  }
+}
+
 // dgamma / dbeta column partials: block (bx, by) covers columns [bx*512, +512) and rows
 // [by*rps, +rps); lane -> 8 columns, wave -> every 4th row.  part: [2][P][d]
 template <bool RMS>
@@ -343,6 +445,64 @@ void dltb_norm_bwd_dgamma(const void* dy, const void* s, const float* mean, cons
     hipLaunchKernelGGL(norm_dgamma_kernel<false>, g2, dim3(256), 0, st, DY, S, mean, rstd, part, N, d, rps);
   hipLaunchKernelGGL(norm_colreduce_kernel, dim3(cdiv(d, 64), rms ? 1 : 2), dim3(256), 0, st, part, P, d,
                      (bf16_t*)gw, rms ? nullptr : (bf16_t*)gb, accumulate);
+}
+
+// ---- fused backward (dx + column partials); rows per wave chosen for >= 256 workgroups
+int dltb_norm_bwd_fused_rpw(int N) {
+  int rpw = N / (kFusedWaves * 256);
+  return rpw < 1 ? 1 : rpw;
+}
+
+int dltb_norm_bwd_fused_blocks(int N) { return cdiv(N, kFusedWaves * dltb_norm_bwd_fused_rpw(N)); }
+
+bool dltb_norm_bwd_fused_supported(int d) { return d % 8 == 0 && nv_for(d) <= 4; }
+
+namespace {
+template <int NV, bool RMS, bool RES, bool DXSUM>
+void launch_bwd_fused(int N, int d, hipStream_t st, const bf16_t* dy, const bf16_t* s, const bf16_t* w,
+                      const float* mean, const float* rstd, const bf16_t* dres, bf16_t* dx, float* part) {
+  const int rpw = dltb_norm_bwd_fused_rpw(N);
+  hipLaunchKernelGGL((norm_bwd_fused_kernel<NV, RMS, RES, DXSUM>), dim3(dltb_norm_bwd_fused_blocks(N)),
+                     dim3(kFusedWaves * 64), (size_t)kFusedWaves * d * sizeof(float), st, dy, s, w, mean, rstd, dres, dx,
+                     part, N, d, rpw);
+}
+template <int NV, bool RMS>
+void launch_bwd_fused_nv(bool res, bool dxsum, int N, int d, hipStream_t st, const bf16_t* dy,
+                         const bf16_t* s, const bf16_t* w, const float* mean, const float* rstd,
+                         const bf16_t* dres, bf16_t* dx, float* part) {
+  if (res) {
+    if (dxsum) launch_bwd_fused<NV, RMS, true, true>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
+    else launch_bwd_fused<NV, RMS, true, false>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
+  } else {
+    if (dxsum) launch_bwd_fused<NV, RMS, false, true>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
+    else launch_bwd_fused<NV, RMS, false, false>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
+  }
+}
+}  // namespace
+
+bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
+                         const float* rstd, const void* dres, void* dx, float* part, int N, int d,
+                         bool rms, bool dxsum, hipStream_t st) {
+  if (!dltb_norm_bwd_fused_supported(d)) return false;
+  auto DY = (const bf16_t*)dy;
+  auto S = (const bf16_t*)s;
+  auto W = (const bf16_t*)w;
+  auto DR = (const bf16_t*)dres;
+  auto DX = (bf16_t*)dx;
+  const bool res = dres != nullptr;
+#define DLTB_NBF(NVV)                                                                                 \
+  do {                                                                                                \
+    if (rms) launch_bwd_fused_nv<NVV, true>(res, dxsum, N, d, st, DY, S, W, mean, rstd, DR, DX, part);  \
+    else launch_bwd_fused_nv<NVV, false>(res, dxsum, N, d, st, DY, S, W, mean, rstd, DR, DX, part);     \
+  } while (0)
+  switch (nv_for(d)) {
+    case 1: DLTB_NBF(1); break;
+    case 2: DLTB_NBF(2); break;
+    case 3: DLTB_NBF(3); break;
+    default: DLTB_NBF(4); break;
+  }
+#undef DLTB_NBF
+  return true;
 }
 
 void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* mean,

@@ -4,6 +4,8 @@
 GEMMs are plain ``torch`` matmuls (hipBLASLt on ROCm); gradient-producing GEMMs write straight
 into the engine's flat gradient slots (``out=`` / ``addmm_``) so no gradient is ever copied.
 """
+import os
+
 import torch
 
 from . import ref
@@ -29,6 +31,9 @@ def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0):
 
 # colpart segment kinds (csrc/colreduce.hip)
 _PLAIN, _GELU, _DROP, _LN, _RMS = 0, 1, 2, 3, 4
+
+# DLTB_FUSED_NORM_BWD=0 restores the two-launch norm backward (dx kernel + colpart partials)
+_FUSED_NORM_BWD = os.environ.get("DLTB_FUSED_NORM_BWD", "1") == "1"
 
 
 class GradReducer:
@@ -64,6 +69,21 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
     column sum of ``src`` -- ``src="dx"`` meaning this call's output) come from ONE colpart launch
     and are reduced at ``red.flush()``."""
     if red is not None:
+        if _gpu(dy) and _FUSED_NORM_BWD and ext().norm_bwd_fused_supported(dy.shape[-1]):
+            # one kernel: dx + gamma / beta partials (+ the column partials of dx itself)
+            C = ext()
+            has_bias = bias is not None and bias[1] is not None
+            dx_sum = has_bias and isinstance(bias[0], str)
+            dx, part = C.norm_bwd_fused(dy, s, w, mean, rstd, dres, rms, dx_sum)
+            red.add(part[0], gw, accumulate)
+            if not rms:
+                red.add(part[1], gb, accumulate)
+            if dx_sum:
+                red.add(part[-1], bias[1], bias[2])
+            elif has_bias:
+                parts = C.colpart([_PLAIN], [bias[0]], [None], [None], [None], [None], 0.0, None, [0])
+                red.add(parts[0][0], bias[1], bias[2])
+            return dx
         if _gpu(dy):
             C = ext()
             dx = C.norm_bwd_dx(dy, s, w, mean, rstd, dres, rms)

@@ -7,6 +7,7 @@ Each linear layer contributes forward (x W^T), dgrad (dY W) and wgrad (dY^T x) p
 layouts the fused Functions issue them.  Prints time, TFLOP/s and the share of the step's GEMM time.
 """
 import argparse
+import itertools
 import os
 import sys
 
@@ -75,17 +76,19 @@ def main():
         if a.dltb:
             from dltb.ops._ext import ext
             C = ext()
-            for cfg in range(6):
-                for sp in ((1, 2, 4, 8) if max(N, K, M) >= 8192 else (1, 2)):
-                    for pf in ((0, 2, 4, 8) if sp == 1 else (0,)):
-                        for gm in ((1, 2, 4, 8) if sp == 1 else (1,)):
-                            tag = f"c{cfg}s{sp}p{pf}g{gm}"
-                            if C.gemm_supported(M, N, K, False, cfg):
-                                kinds.append((f"fwd[{tag}]", lambda cfg=cfg, sp=sp, pf=pf, gm=gm: C.gemm(x, w, y, None, False, False, sp, cfg, pf, gm)))
-                            if C.gemm_supported(M, K, N, False, cfg):
-                                kinds.append((f"dgT[{tag}]", lambda cfg=cfg, sp=sp, pf=pf, gm=gm: C.gemm(dy, wT, dx, None, False, False, sp, cfg, pf, gm)))
-                            if C.gemm_supported(N, K, M, True, cfg):
-                                kinds.append((f"wg[{tag}]", lambda cfg=cfg, sp=sp, pf=pf, gm=gm: C.gemm(dy, x, dw, None, True, False, sp, cfg, pf, gm)))
+            splits = (1, 2, 4, 8) if max(N, K, M) >= 8192 else (1, 2, 4)
+            for cfg, sp, gm, stg in itertools.product(range(6), splits, (1, 4), (0, 2)):
+                if gm > 1 and sp > 1:
+                    continue
+                pf = 0
+                tag = f"c{cfg}s{sp}g{gm}n{stg}"
+                kw = dict(splits=sp, cfg=cfg, pf=pf, gm=gm, stages=stg)
+                if C.gemm_supported(M, N, K, False, cfg):
+                    kinds.append((f"fwd[{tag}]", lambda kw=kw: C.gemm(x, w, y, None, False, False, **kw)))
+                if C.gemm_supported(M, K, N, False, cfg):
+                    kinds.append((f"dgT[{tag}]", lambda kw=kw: C.gemm(dy, wT, dx, None, False, False, **kw)))
+                if C.gemm_supported(N, K, M, True, cfg):
+                    kinds.append((f"wg[{tag}]", lambda kw=kw: C.gemm(dy, x, dw, None, True, False, **kw)))
         if a.layouts:
             kinds += [("dgradT", lambda: torch.mm(dy, wT.t(), out=dx)),     # W^T cached: NT form
                       ("wgradT", lambda: torch.mm(dyT, xT.t(), out=dw))]    # activations transposed

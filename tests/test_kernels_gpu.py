@@ -150,6 +150,43 @@ def test_batched_column_reductions(N):
     close(outs[5], dm.float().sum(0), 0.5, 2e-2, "dropout bias")
 
 
+@pytest.mark.parametrize("N,d", [(2048, 1024), (300, 768), (4096, 2048), (64, 64)])
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("bias_src", [None, "dx", "ext"])
+def test_norm_bwd_fused(N, d, rms, bias_src):
+    """One-launch norm backward (dx + gamma / beta partials + column partials of dx) through
+    functional.norm_bwd vs an fp32 torch reference; the dqkv-style external bias source too."""
+    from dltb.ops import functional as F_
+    C = ext()
+    assert C.norm_bwd_fused_supported(d)
+    dy, s_, dres = rnd(N, d), rnd(N, d), rnd(N, d)
+    w = rnd(d, scale=0.5) + 1
+    mean = None if rms else torch.randn(N, device=DEV) * 0.1
+    rstd = torch.rand(N, device=DEV) + 0.5
+    gw = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
+    gb = None if rms else torch.full((d,), 1.0, device=DEV, dtype=torch.bfloat16)
+    ext_src = rnd(N, 3 * d) if bias_src == "ext" else None
+    bslot = torch.zeros(3 * d if bias_src == "ext" else d, device=DEV, dtype=torch.bfloat16)
+    bias = None if bias_src is None else (("dx" if bias_src == "dx" else ext_src), bslot, False)
+    red = F_.GradReducer()
+    dx = F_.norm_bwd(dy, s_, w, mean, rstd, dres, gw, gb, gb is not None, rms, red=red, bias=bias)
+    red.flush()
+    x32 = s_.float()
+    xh = (x32 - (0.0 if rms else mean[:, None])) * rstd[:, None]
+    g = dy.float() * w.float()
+    s1 = 0.0 if rms else g.mean(-1, keepdim=True)
+    s2 = (g * xh).mean(-1, keepdim=True)
+    rdx = rstd[:, None] * (g - s1 - xh * s2) + dres.float()
+    close(dx, rdx, 3e-2, 3e-2, "dx")
+    close(gw, (dy.float() * xh).sum(0), 0.5, 2e-2, "dgamma")
+    if not rms:
+        close(gb, dy.float().sum(0) + 1.0, 0.5, 2e-2, "dbeta (accumulate)")
+    if bias_src == "dx":
+        close(bslot, dx.float().sum(0), 0.5, 2e-2, "dx column sum")
+    elif bias_src == "ext":
+        close(bslot, ext_src.float().sum(0), 0.5, 2e-2, "external column sum")
+
+
 @pytest.mark.parametrize("R,C", [(1024, 3072), (4096, 1024), (100, 36)])
 def test_transpose_into(R, C):
     C_ = ext()
@@ -176,10 +213,10 @@ def test_sumsq_is_deterministic():
                                                (512, 256, 256, 1, 1), (256, 512, 192, 2, 2),
                                                (256, 192, 512, 3, 1), (192, 256, 320, 4, 2),
                                                (192, 320, 256, 5, 1)])
-@pytest.mark.parametrize("pf,gm", [(0, 1), (3, 2)])
-def test_gemm(tn, M, N, K, cfg, splits, pf, gm):
+@pytest.mark.parametrize("pf,gm,stages", [(0, 1, 0), (3, 2, 0), (0, 1, 2)])
+def test_gemm(tn, M, N, K, cfg, splits, pf, gm, stages):
     """dltb GEMM (NT: a[M,K] b[N,K]; TN: a[K,M] b[K,N]) vs fp32 torch, incl. bias / accumulate /
-    split-K and row-strided operand views."""
+    split-K, row-strided operand views and the double-buffered (two workgroups / CU) variant."""
     C_ = ext()
     if not C_.gemm_supported(M, N, K, tn, cfg):
         pytest.skip("tile config not offered for this layout")
@@ -192,11 +229,11 @@ def test_gemm(tn, M, N, K, cfg, splits, pf, gm):
         a, b = a_full[:, :K], b_full
         ref32 = a.float() @ b.float().t()
     bias = rnd(N)
-    out = C_.gemm(a, b, None, bias, tn, False, splits, cfg, pf, gm)
+    out = C_.gemm(a, b, None, bias, tn, False, splits, cfg, pf, gm, stages=stages)
     close(out, ref32 + bias.float(), 0.1, 2e-2, "gemm + bias")
     prev = rnd(M, N)
     acc = prev.clone()
-    C_.gemm(a, b, acc, None, tn, True, splits, cfg, pf, gm)
+    C_.gemm(a, b, acc, None, tn, True, splits, cfg, pf, gm, stages=stages)
     close(acc, ref32 + prev.float(), 0.1, 2e-2, "gemm accumulate")
 
 
