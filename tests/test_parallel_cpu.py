@@ -118,13 +118,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, strategy, accum, kw, out_path):
+def _worker(rank, world, port, strategy, accum, kw, out_path, global_batch=4):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.set_num_threads(1)
-        sd = _train(strategy, _batches(STEPS, 4), rank, world, accum, **kw)
+        sd = _train(strategy, _batches(STEPS, global_batch), rank, world, accum, **kw)
         if rank == 0:
             torch.save(sd, out_path)
     finally:
@@ -153,6 +153,20 @@ def test_world2_matches_single_process(strategy, accum, kw):
     for n in ref:
         assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
 
+
+@pytest.mark.parametrize("strategy,accum,kw", [("zero2", 2, {}), ("zero3", 2, {}), ("ddp", 1, {}),
+                                               ("fsdp", 1, {})])
+def test_world4_matches_single_process(strategy, accum, kw):
+    """Four ranks (uneven bucket chunks, padding on every rank, prefetch across 4 shards) reproduce
+    the single-process run on the same global batch -- the rank layout of the 4-GPU baseline."""
+    world, gb = 4, 8
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "sd.pt")
+        mp.spawn(_worker, args=(world, _free_port(), strategy, accum, dict(kw), out, gb), nprocs=world, join=True)
+        got = torch.load(out, weights_only=True)
+    ref = _train(strategy, _batches(STEPS, gb), 0, 1, accum, **dict(kw))
+    for n in ref:
+        assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
 
 
 def _worker_defer(rank, world, port, out_path):
