@@ -260,7 +260,7 @@ def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal,
         C = ext()
         delta = C.attn_bwd_delta(o, do, B, T, Hq)
         m = aux if p > 0 else None
-        if par is not None and par.enabled:
+        if par is not None and par.enabled and par.attn:
             with par.fork(q, k, v, do, lse, delta, m):
                 C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p)
         else:
@@ -287,7 +287,7 @@ def linear_dgrad(dy2d, w, wt=None):
 def linear_wgrad(dy2d, x2d, dw, db, accumulate, par=None):
     """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy).  With ``par`` the
     work runs on the side stream (parameter gradients are off the critical path)."""
-    if par is not None and par.enabled:
+    if par is not None and par.enabled and par.wgrad:
         with par.fork(dy2d, x2d):
             linear_wgrad(dy2d, x2d, dw, db, accumulate)
         return
