@@ -68,12 +68,17 @@ class FlatLayout:
 
 
 def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 0,
-                align: int = ALIGN, shard: bool = False, param_filter=None) -> FlatLayout:
+                align: int = ALIGN, shard: bool = False, param_filter=None,
+                solo_tail: int = 0) -> FlatLayout:
     """Lay ``units`` (already in the desired memory order) out in one flat buffer.
 
     ``bucket_elems``: close a bucket once it holds at least this many elements (0 = one bucket per
     unit).  ``shard``: pad each bucket to ``world_size * align`` for equal reduce-scatter chunks.
     ``param_filter(unit, i) -> bool`` restricts which parameters are placed (ZeRO-3 persistence).
+    ``solo_tail``: the last ``solo_tail`` units get a bucket each.  In backward order these are the
+    units that finish last (block 0, the tied embedding): their collectives cannot overlap any
+    compute, so keeping them out of a large shared bucket shortens the exposed communication tail
+    (a 64 MiB bucket of blocks 2..0 + the embedding would start only after the embedding).
     """
     slots: Dict[Tuple[int, int], ParamSlot] = {}
     buckets: List[Bucket] = []
@@ -88,7 +93,11 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
         b.chunk = (b.end - b.start) // world_size if shard else 0
         return b.end
 
-    for u in units:
+    tail_from = len(units) - max(0, int(solo_tail))
+    for ui, u in enumerate(units):
+        if ui >= tail_from and cur is not None:
+            off = close(cur)
+            cur = None
         placed = False
         for i, p in enumerate(u.params):
             if param_filter is not None and not param_filter(u, i):
@@ -107,7 +116,7 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
         if placed:
             cur.units.append(u)
             unit_bucket[id(u)] = cur.index
-            if bucket_elems <= 0 or cur.end - cur.start >= bucket_elems:
+            if bucket_elems <= 0 or cur.end - cur.start >= bucket_elems or ui >= tail_from:
                 off = close(cur)
                 cur = None
     if cur is not None:

@@ -6,10 +6,11 @@ DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
 * Parameters: ONE flat bf16 buffer in backward order (head, block L-1 ... block 0, embedding), every
   ``nn.Parameter`` a view into it.  Gradients: a flat bf16 buffer with the same layout, written in
   place by the fused block backward (no autograd hooks, no bucket copies).
-* Buckets: consecutive units grouped up to ``bucket_mb`` (xGMI-tuned default 64 MiB).  When the
-  last unit of a bucket finishes its backward the engine launches the bucket's collective
-  immediately (async, on the process group's stream) so communication overlaps the remaining
-  backward.
+* Buckets: consecutive units grouped up to ``bucket_mb`` (xGMI-tuned default 64 MiB); the last two
+  units of the backward (block 0 and the embedding) get a bucket each, so the collective that no
+  compute can hide is only the embedding's.  When the last unit of a bucket finishes its backward
+  the engine launches the bucket's collective immediately (async, on the process group's stream)
+  so communication overlaps the remaining backward.
 * DDP (``zero_stage=0``): SUM all-reduce per bucket; the 1/world average is folded into the fused
   AdamW's gradient scale.  fp32 master / Adam moments for the whole model on every rank.
 * ZeRO-2: reduce-scatter per bucket, every micro-step, into this rank's chunk; chunks accumulate
@@ -41,7 +42,8 @@ class ReplicatedEngine(Engine):
         if ds_cap:
             bucket_elems = min(bucket_elems, int(ds_cap)) if bucket_elems else int(ds_cap)
         shard = self.stage >= 1
-        self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard)
+        self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
+                                      solo_tail=int(cfg.extra.get("solo_tail_units", 2)))
         dev, dt = self.device, self.compute_dtype
         master_full = torch.zeros(L.total, dtype=torch.float32, device=dev)
         for s in L.slots.values():
