@@ -47,10 +47,19 @@ const int64_t* seed_ptr(const optional<Tensor>& seed, double p) {
   return seed->data_ptr<int64_t>();
 }
 
+// caller-provided output (a view of a preallocated, layer-strided activation buffer) or a new tensor
+Tensor out_or_new(const optional<Tensor>& out, const Tensor& like, const char* name) {
+  if (!out.has_value()) return at::empty_like(like);
+  check_contig_bf16(*out, name);
+  TORCH_CHECK(out->sizes() == like.sizes(), name, ": output shape");
+  check_align16(*out, name);
+  return *out;
+}
+
 // ------------------------------------------------------------------------------------ norms
 std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& r, const Tensor& w,
                              const optional<Tensor>& b, double eps, bool rms, double p,
-                             const optional<Tensor>& seed, int64_t site) {
+                             const optional<Tensor>& seed, int64_t site, const optional<Tensor>& y_out) {
   check_contig_bf16(x, "x");
   check_contig_bf16(w, "w");
   const int64_t d = x.size(-1);
@@ -68,7 +77,7 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const optional<Tensor>& r, const T
     TORCH_CHECK(r->sizes() == x.sizes(), "norm: residual shape");
     s = at::empty_like(x);
   }
-  auto y = at::empty_like(x);
+  auto y = out_or_new(y_out, x, "norm_fwd y_out");
   auto fopt = x.options().dtype(at::kFloat);
   auto mean = rms ? Tensor() : at::empty({N}, fopt);
   auto rstd = at::empty({N}, fopt);
@@ -113,10 +122,10 @@ Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const option
 }
 
 // ------------------------------------------------------------------------------ elementwise
-Tensor gelu_fwd(const Tensor& f) {
+Tensor gelu_fwd(const Tensor& f, const optional<Tensor>& out) {
   check_contig_bf16(f, "f");
   TORCH_CHECK(f.numel() % 8 == 0, "gelu: numel % 8");
-  auto g = at::empty_like(f);
+  auto g = out_or_new(out, f, "gelu_fwd out");
   dltb_gelu_fwd(f.data_ptr(), g.data_ptr(), f.numel(), cur_stream());
   return g;
 }
@@ -413,7 +422,8 @@ Tensor attn_mask(int64_t B, int64_t T, int64_t Hq, double p, const Tensor& seed,
 
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v,
                              const optional<Tensor>& mask, int64_t B, int64_t T, int64_t Hq,
-                             int64_t Hkv, double scale, bool causal, double p) {
+                             int64_t Hkv, double scale, bool causal, double p,
+                             const optional<Tensor>& o_out) {
   const int64_t D = attn_head_dim(q, B, T, Hq);
   TORCH_CHECK(Hq % Hkv == 0, "attention: Hq % Hkv");
   check_attn_view(q, "q", B * T, Hq, D);
@@ -422,7 +432,14 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v,
   const uint32_t thr = thr_of(p);
   const uint32_t* mp = mask_ptr(mask, thr, B, T, Hq);
   dltb_attn_init_attributes();
-  auto o = at::empty({B * T, Hq * D}, q.options());
+  Tensor o;
+  if (o_out.has_value()) {
+    check_contig_bf16(*o_out, "attn_fwd o_out");
+    TORCH_CHECK(o_out->dim() == 2 && o_out->size(0) == B * T && o_out->size(1) == Hq * D, "attn_fwd o_out shape");
+    o = *o_out;
+  } else {
+    o = at::empty({B * T, Hq * D}, q.options());
+  }
   auto lse = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
   dltb_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), mp,
                 q.stride(0), k.stride(0), v.stride(0), o.stride(0), (int)B, (int)T, (int)Hq, (int)Hkv,
@@ -502,7 +519,8 @@ Tensor norm_bwd_dx(const Tensor& dy, const Tensor& s, const Tensor& w, const opt
 // fused norm backward: (dx, part[K, P, d] f32) with K = (rms ? 1 : 2) + dx_sum; see norm.hip
 std::tuple<Tensor, Tensor> norm_bwd_fused(const Tensor& dy, const Tensor& s, const Tensor& w,
                                           const optional<Tensor>& mean, const Tensor& rstd,
-                                          const optional<Tensor>& dres, bool rms, bool dx_sum) {
+                                          const optional<Tensor>& dres, bool rms, bool dx_sum,
+                                          const optional<Tensor>& dx_out) {
   check_contig_bf16(dy, "dy");
   check_contig_bf16(s, "s");
   check_contig_bf16(w, "w");
@@ -515,7 +533,7 @@ std::tuple<Tensor, Tensor> norm_bwd_fused(const Tensor& dy, const Tensor& s, con
     check_contig_bf16(*dres, "dres");
     TORCH_CHECK(dres->sizes() == dy.sizes(), "norm_bwd_fused: dres shape");
   }
-  auto dx = at::empty_like(dy);
+  auto dx = out_or_new(dx_out, dy, "norm_bwd_fused dx_out");
   const int64_t K = (rms ? 1 : 2) + (dx_sum ? 1 : 0);
   auto part = at::empty({K, (int64_t)dltb_norm_bwd_fused_blocks((int)N), d}, dy.options().dtype(at::kFloat));
   dltb_norm_bwd_fused(dy.data_ptr(), s.data_ptr(), w.data_ptr(), rms ? nullptr : mean->data_ptr<float>(),
@@ -696,9 +714,10 @@ Tensor gemm(const Tensor& a, const Tensor& b, const optional<Tensor>& out, const
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dltb gfx950 (MI355X) HIP kernels";
-  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_fwd", &norm_fwd, py::arg("x"), py::arg("r"), py::arg("w"), py::arg("b"), py::arg("eps"),
+        py::arg("rms"), py::arg("p"), py::arg("seed"), py::arg("site"), py::arg("y_out") = py::none());
   m.def("norm_bwd", &norm_bwd);
-  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_fwd", &gelu_fwd, py::arg("f"), py::arg("out") = py::none());
   m.def("gelu_bwd", &gelu_bwd);
   m.def("colsum_into", &colsum_into);
   m.def("dropout", &dropout);
@@ -714,13 +733,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_", &sumsq_);
   m.def("clip_coef", &clip_coef);
   m.def("attn_mask", &attn_mask);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"), py::arg("B"),
+        py::arg("T"), py::arg("Hq"), py::arg("Hkv"), py::arg("scale"), py::arg("causal"), py::arg("p"),
+        py::arg("o_out") = py::none());
   m.def("attn_bwd_delta", &attn_bwd_delta);
   m.def("attn_bwd_part", &attn_bwd_part);
   m.def("attn_bwd", &attn_bwd);
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
-  m.def("norm_bwd_fused", &norm_bwd_fused);
+  m.def("norm_bwd_fused", &norm_bwd_fused, py::arg("dy"), py::arg("s"), py::arg("w"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dres"), py::arg("rms"), py::arg("dx_sum"), py::arg("dx_out") = py::none());
   m.def("norm_bwd_fused_supported", [](int64_t d) { return dltb_norm_bwd_fused_supported((int)d); });
   m.def("colpart", &colpart);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias"), py::arg("tn"),

@@ -22,6 +22,7 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
+from types import SimpleNamespace
 
 import torch
 import torch.nn as nn
@@ -104,20 +105,21 @@ class _BlockFn(torch.autograd.Function):
         H, d = cfg.n_head, cfg.n_embd
         p = model.drop_p
         par = GradStreams(x.device, enabled=_MASK_STREAM or None)
+        lb = model.layer_buffer(i)          # layer-strided GEMM operands (batched weight gradients)
         amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x, par)   # overlaps LN1 + QKV GEMM
-        _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False)
+        _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False, y_out=lb and lb.h1)
         qkv = F_.linear_fwd(h1, win, bin_)
         o, lse, amask = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
                                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i),
-                                    amask, par)
+                                    amask, par, o_out=lb and lb.o)
         a = F_.linear_fwd(o, wo, bo)
-        x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False)
+        x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
         f = F_.linear_fwd(h2, w1, b1)
-        g = F_.gelu_fwd(f)
+        g = F_.gelu_fwd(f, out=lb and lb.g)
         m = F_.linear_fwd(g, w2, b2)
         x2 = F_.dropout(x1, m, p, rt.seed, model.site_mlp(i))
         rt.release_forward(unit)
-        ctx.model, ctx.i = model, i
+        ctx.model, ctx.i, ctx.lb = model, i, lb
         ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g)
         return x2
 
@@ -134,26 +136,35 @@ class _BlockFn(torch.autograd.Function):
         p = model.drop_p
         dx2 = dx2.contiguous()
         s = [rt.grad_slot(unit, j) for j in range(12)]
-        par = GradStreams(dx2.device)      # parameter-gradient work -> side stream
+        lb = ctx.lb
+        par = GradStreams(dx2.device)      # parameter-gradient work -> side stream (DLTB_SIDE_STREAM)
+
+        def wgrad(j, dy, xin):             # dW_j (+)= dy^T xin: now, or queued and batched by the engine
+            if par.enabled and par.wgrad:
+                F_.linear_wgrad(dy, xin, s[j][0], None, s[j][1], par)
+            else:
+                rt.wgrad(unit, j, dy, xin, s[j][0], s[j][1])
+
         red = F_.GradReducer()   # the 8 bias / LayerNorm column sums: fused partials, ONE reduce launch
         # MLP
-        dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red)
-        F_.linear_wgrad(dm, g, s[10][0], None, s[10][1], par)
+        dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
+                                 out=lb and lb.dm)
+        wgrad(10, dm, g)
         dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
-        df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red)
-        F_.linear_wgrad(df, h2, s[8][0], None, s[8][1], par)
+        df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
+        wgrad(8, df, h2)
         dh2 = F_.linear_dgrad(df, w1, rt.weight_t(unit, 8, w1))
         dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False, par,
-                          red, bias=("dx", s[5][0], s[5][1]))
+                          red, bias=("dx", s[5][0], s[5][1]), dx_out=lb and lb.dx1)
         # attention
-        F_.linear_wgrad(dx1, o, s[4][0], None, s[4][1], par)
+        wgrad(4, dx1, o)
         do = F_.linear_dgrad(dx1, wo, rt.weight_t(unit, 4, wo))
-        dqkv = torch.empty_like(qkv)
+        dqkv = torch.empty_like(qkv) if lb is None else lb.dqkv
         F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, amask,
                     dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i), par)
         par.join()                                            # dQ (side) completes dqkv
-        F_.linear_wgrad(dqkv, h1, s[2][0], None, s[2][1], par)
+        wgrad(2, dqkv, h1)
         dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False, par,
                          red, bias=(dqkv, s[3][0], s[3][1]))
@@ -233,6 +244,8 @@ class TinyGPT(nn.Module):
         self.apply(self._init_weights)
         self.rt = EAGER
         self.drop_p = cfg.dropout
+        self._lbufs = None
+        self._lbuf_key = None
         self._build_units()
 
     @staticmethod
@@ -274,6 +287,32 @@ class TinyGPT(nn.Module):
     def num_params(self):
         return sum(p.numel() for p in self.parameters())
 
+    def _prepare_layer_buffers(self, N, like):
+        """Under an engine that batches weight gradients (``rt.defer_wgrad``), the GEMM operands of
+        every block's dW products live in layer-strided buffers [L, N, k] -- row L-1-i for block i,
+        the order of the blocks' gradient slots in the flat buffer -- so a group of blocks is one
+        strided-batched GEMM (parallel/wgrad.py).  X: ln_1 / ln_2 outputs, attention output, GELU
+        output; dY: dqkv, d(x1), d(fc1 pre-activation), d(fc2 output).  ~1 GB at TinyGPT-A."""
+        if not (getattr(self.rt, "defer_wgrad", False) and self.training and torch.is_grad_enabled()):
+            self._lbufs, self._lbuf_key = None, None
+            return
+        L, d, F = self.cfg.n_layer, self.cfg.n_embd, 4 * self.cfg.n_embd
+        key = (L, N, d, like.dtype, like.device)
+        if self._lbuf_key != key:
+            mk = lambda k: torch.empty(L, N, k, dtype=like.dtype, device=like.device)  # noqa: E731
+            self._lbufs = SimpleNamespace(h1=mk(d), o=mk(d), h2=mk(d), g=mk(F), dqkv=mk(3 * d), dx1=mk(d),
+                                          df=mk(F), dm=mk(d))
+            self._lbuf_key = key
+        self._lbuf_on = True
+
+    def layer_buffer(self, i):
+        """Views of block ``i``'s row of the layer-strided buffers, or None (immediate dW)."""
+        b = self._lbufs
+        if b is None or not getattr(self, "_lbuf_on", False):
+            return None
+        r = self.cfg.n_layer - 1 - i
+        return SimpleNamespace(**{k: v[r] for k, v in vars(b).items()})
+
     def forward(self, idx, targets=None, return_logits=False):
         B, T = idx.shape
         assert T <= self.cfg.block_size, f"Sequence {T} exceeds block size {self.cfg.block_size}"
@@ -284,6 +323,8 @@ class TinyGPT(nn.Module):
             self.drop_p = self.cfg.dropout
         if self.drop_p > 0 and self.rt.seed is None:
             raise RuntimeError("dropout needs a StepSeed on the runtime (engine.attach or rt.seed = ...)")
+        self._lbuf_on = False
+        self._prepare_layer_buffers(B * T, self.transformer["wte"].weight)
         anchor = torch.empty((), requires_grad=True)    # graph entry (CPU scalar, never updated)
         x = _EmbedFn.apply(anchor, idx, self)
         for i in range(len(self.unit_blocks)):

@@ -21,12 +21,22 @@ def _sd(seed):
 
 
 # ------------------------------------------------------------------------------ norms
-def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0):
-    """Returns (s, y, mean, rstd); s = x + dropout(r) when r is given (else None)."""
+def _into(out, t):
+    """CPU path of an op with a caller-provided output: copy the reference result into it."""
+    if out is None:
+        return t
+    out.copy_(t)
+    return out
+
+
+def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0, y_out=None):
+    """Returns (s, y, mean, rstd); s = x + dropout(r) when r is given (else None).  ``y_out``: write
+    y into this (layer-strided activation buffer) view."""
     if _gpu(x):
-        s, y, mean, rstd = ext().norm_fwd(x, r, w, b, eps, rms, p, _sd(seed) if p > 0 else None, site)
+        s, y, mean, rstd = ext().norm_fwd(x, r, w, b, eps, rms, p, _sd(seed) if p > 0 else None, site, y_out)
         return (s if r is not None else None), y, (None if rms else mean), rstd
-    return ref.norm_fwd(x, r, w, b, eps, rms, p, seed, site)
+    s, y, mean, rstd = ref.norm_fwd(x, r, w, b, eps, rms, p, seed, site)
+    return s, _into(y_out, y), mean, rstd
 
 
 # colpart segment kinds (csrc/colreduce.hip)
@@ -62,7 +72,8 @@ class GradReducer:
             self.parts, self.outs, self.acc = [], [], []
 
 
-def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=None, bias=None):
+def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=None, bias=None,
+             dx_out=None):
     """dx on the current stream; dgamma/dbeta (parameter gradients) on ``par``'s side stream.
 
     With a :class:`GradReducer` the dgamma/dbeta partials (and, with ``bias=(src, slot, acc)``, the
@@ -74,7 +85,7 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
             C = ext()
             has_bias = bias is not None and bias[1] is not None
             dx_sum = has_bias and isinstance(bias[0], str)
-            dx, part = C.norm_bwd_fused(dy, s, w, mean, rstd, dres, rms, dx_sum)
+            dx, part = C.norm_bwd_fused(dy, s, w, mean, rstd, dres, rms, dx_sum, dx_out)
             red.add(part[0], gw, accumulate)
             if not rms:
                 red.add(part[1], gb, accumulate)
@@ -86,7 +97,7 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
             return dx
         if _gpu(dy):
             C = ext()
-            dx = C.norm_bwd_dx(dy, s, w, mean, rstd, dres, rms)
+            dx = _into(dx_out, C.norm_bwd_dx(dy, s, w, mean, rstd, dres, rms))
             kinds, a, b, mn, rs = [_RMS if rms else _LN], [dy], [s], [mean], [rstd]
             if bias is not None and bias[1] is not None:
                 src = dx if isinstance(bias[0], str) else bias[0]
@@ -98,7 +109,7 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
             if len(parts) > 1:
                 red.add(parts[1][0], bias[1], bias[2])
             return dx
-        dx = ref.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
+        dx = _into(dx_out, ref.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms))
         if bias is not None and bias[1] is not None:
             ref.colsum_into(dx if isinstance(bias[0], str) else bias[0], bias[1], bias[2])
         return dx
@@ -114,30 +125,30 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
 
 
 # ------------------------------------------------------------------------------ elementwise
-def gelu_fwd(f):
-    return ext().gelu_fwd(f) if _gpu(f) else ref.gelu_fwd(f)
+def gelu_fwd(f, out=None):
+    return ext().gelu_fwd(f, out) if _gpu(f) else _into(out, ref.gelu_fwd(f))
 
 
-def gelu_bwd(dg, f, db, accumulate, red=None):
+def gelu_bwd(dg, f, db, accumulate, red=None, out=None):
     """df = dg * gelu'(f); the fc1 bias gradient colsum(df) is fused (reduced at red.flush())."""
     if _gpu(dg):
         if red is None:
-            return ext().gelu_bwd(dg, f, db, accumulate)
-        df = torch.empty_like(dg)
+            return _into(out, ext().gelu_bwd(dg, f, db, accumulate))
+        df = torch.empty_like(dg) if out is None else out
         parts = ext().colpart([_GELU], [dg], [f], [df], [None], [None], 0.0, None, [0])
         red.add(parts[0][0], db, accumulate)
         return df
-    return ref.gelu_bwd(dg, f, db, accumulate)
+    return _into(out, ref.gelu_bwd(dg, f, db, accumulate))
 
 
-def dropout_bwd_bias(g, p, seed, site, db, accumulate, red):
+def dropout_bwd_bias(g, p, seed, site, db, accumulate, red, out=None):
     """dm = dropout_mask(g) / (1-p) (the Dropout backward) with colsum(dm) -> db fused."""
     if _gpu(g):
-        dm = torch.empty_like(g)
+        dm = torch.empty_like(g) if out is None else out
         parts = ext().colpart([_DROP], [g], [None], [dm], [None], [None], p, _sd(seed) if p > 0 else None, [site])
         red.add(parts[0][0], db, accumulate)
         return dm
-    dm = ref.dropout(None, g, p, seed, site)
+    dm = _into(out, ref.dropout(None, g, p, seed, site))
     if db is not None:
         ref.colsum_into(dm, db, accumulate)
     return dm
@@ -240,17 +251,17 @@ def attn_mask(B, T, Hq, p, seed, site, like, par=None):
     return ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, like)
 
 
-def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site, mask=None, par=None):
+def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site, mask=None, par=None, o_out=None):
     """Returns (o, lse, aux); ``aux`` (the packed dropout mask on the GPU) goes back into attn_bwd."""
     if _gpu(q):
         if p > 0 and mask is None:
             mask = ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, q)
         if par is not None:
             par.join()                      # the mask was produced on the side stream
-        o, lse = ext().attn_fwd(q, k, v, mask if p > 0 else None, B, T, Hq, Hkv, scale, causal, p)
+        o, lse = ext().attn_fwd(q, k, v, mask if p > 0 else None, B, T, Hq, Hkv, scale, causal, p, o_out)
         return o, lse, (mask if p > 0 else None)
     o, lse = ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site)
-    return o, lse, None
+    return _into(o_out, o), lse, None
 
 
 def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site, par=None):

@@ -27,6 +27,7 @@ from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
 from .engine import Engine
 from .flat import ALIGN, owner_segments, plan_layout
+from .wgrad import WgradQueue
 
 
 class ReplicatedEngine(Engine):
@@ -79,6 +80,10 @@ class ReplicatedEngine(Engine):
         self._cache_wt = bool(cfg.extra.get("cache_weight_t", os.environ.get("DLTB_CACHE_WT", "1") == "1"))
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
+        # weight gradients queued and issued as strided-batched GEMMs (parallel/wgrad.py): world 1
+        # flushes once per backward, world > 1 per bucket right before its collective
+        self.defer_wgrad = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
+        self._wq = WgradQueue()
         self._launched = [False] * len(L.buckets)
         nbytes = L.total * elem
         if self.world > 1:
@@ -125,13 +130,22 @@ class ReplicatedEngine(Engine):
             return True
         return self._is_boundary
 
+    def wgrad(self, unit, i, dy, x, dw, accumulate):
+        if self.defer_wgrad:
+            self._wq.add(unit, i, dy, x, dw, accumulate)
+        else:
+            super().wgrad(unit, i, dy, x, dw, accumulate)
+
     def grads_ready(self, unit):
         b = self._bucket_of.get(id(unit))
         if b is None:
             return
         self._pending[b] -= 1
-        if self._pending[b] == 0 and self._reduce_now():
-            self._launch(b)
+        if self._pending[b] == 0:
+            if self.world > 1:
+                self._wq.flush(self.layout.buckets[b].units)    # this bucket's dW, then its collective
+            if self._reduce_now():
+                self._launch(b)
 
     def _launch(self, b):
         bk = self.layout.buckets[b]
@@ -148,6 +162,7 @@ class ReplicatedEngine(Engine):
             self._written.clear()         # the full gradient buffer is reduced every micro-step
 
     def _finish_backward(self):
+        self._wq.flush()                                        # world 1: every block in one batch
         if self._reduce_now():
             for b, done in enumerate(self._launched):   # units that never reported (unused params)
                 if not done:

@@ -7,7 +7,8 @@ the runtime instead of to ``nn.Parameter.grad``:
     forward : params = rt.acquire(unit)            ... compute ...   rt.release_forward(unit)
     backward: params = rt.acquire_backward(unit)   (re-gathers / prefetches under FSDP, ZeRO-3)
               slot, acc = rt.grad_slot(unit, i)    (flat-buffer gradient view + overwrite/accumulate)
-              ... GEMMs write dW straight into the slots ...
+              ... GEMMs write dW straight into the slots (rt.wgrad: now, or queued and batched
+                  over blocks by engines that defer them) ...
               rt.grads_ready(unit)                 (DDP: bucket all-reduce; ZeRO/FSDP: reduce-scatter)
               rt.release_backward(unit)
 
@@ -80,6 +81,16 @@ class ParamRuntime:
             p.grad = torch.empty_like(p)
             return p.grad, False
         return p.grad, True
+
+    # weight gradients (dW (+)= dY^T X of a linear layer)
+    defer_wgrad = False     # True: the engine queues them (parallel/wgrad.py) and issues batches
+
+    def wgrad(self, unit: Unit, i: int, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
+              accumulate: bool):
+        """Write ``dy^T x`` into gradient slot ``dw`` (``accumulate``: add).  The default issues it
+        now; engines with ``defer_wgrad`` run it later, batched with the other blocks' products."""
+        from ..ops import functional as F_
+        F_.linear_wgrad(dy, x, dw, None, accumulate)
 
     def grads_ready(self, unit: Unit):
         pass
