@@ -289,9 +289,10 @@ class TinyGPT(nn.Module):
 
     def _prepare_layer_buffers(self, N, like):
         """Under an engine that batches weight gradients (``rt.defer_wgrad``), the GEMM operands of
-        every block's dW products live in layer-strided buffers [L, N, k] -- row L-1-i for block i,
+        every block's dW products live in layer-strided buffers [L, N, k] -- one row per block, in
         the order of the blocks' gradient slots in the flat buffer -- so a group of blocks is one
-        strided-batched GEMM (parallel/wgrad.py).  X: ln_1 / ln_2 outputs, attention output, GELU
+        strided-batched GEMM (parallel/wgrad.py); the row order follows the engine's slot order
+        (``rt.wgrad_rows_reversed``).  X: ln_1 / ln_2 outputs, attention output, GELU
         output; dY: dqkv, d(x1), d(fc1 pre-activation), d(fc2 output).  ~1 GB at TinyGPT-A."""
         if not (getattr(self.rt, "defer_wgrad", False) and self.training and torch.is_grad_enabled()):
             self._lbufs, self._lbuf_key = None, None
@@ -310,7 +311,7 @@ class TinyGPT(nn.Module):
         b = self._lbufs
         if b is None or not getattr(self, "_lbuf_on", False):
             return None
-        r = self.cfg.n_layer - 1 - i
+        r = self.cfg.n_layer - 1 - i if getattr(self.rt, "wgrad_rows_reversed", True) else i
         return SimpleNamespace(**{k: v[r] for k, v in vars(b).items()})
 
     def forward(self, idx, targets=None, return_logits=False):

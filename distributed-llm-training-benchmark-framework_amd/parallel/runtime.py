@@ -84,6 +84,9 @@ class ParamRuntime:
 
     # weight gradients (dW (+)= dY^T X of a linear layer)
     defer_wgrad = False     # True: the engine queues them (parallel/wgrad.py) and issues batches
+    # order of the blocks' gradient slots in the engine's flat buffer: True = last block first
+    # (backward-ordered replicated layouts); the model's layer-strided buffers follow it
+    wgrad_rows_reversed = True
 
     def wgrad(self, unit: Unit, i: int, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
               accumulate: bool):

@@ -23,12 +23,15 @@ MI355X-native design on ``torch.distributed`` (RCCL over xGMI):
 * Optimizer: one fused AdamW launch over the rank's owner space [persistent chunk | group shards];
   the bf16 shard is written in place and becomes the next all-gather's input.
 """
+import os
+
 import torch
 
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
 from .engine import Engine
 from .flat import ALIGN, plan_layout
+from .wgrad import WgradQueue
 
 _HUGE = 1 << 62
 
@@ -150,11 +153,38 @@ class ShardedEngine(Engine):
                                if any(self._persistent(u, i) for i in range(len(u.params)))])
         self._p_left = self._p_pending
         self._held_grads = []
+        # single process: the dW products of all blocks run as strided-batched GEMMs at the end of
+        # backward (parallel/wgrad.py); with shards, each group's gradient is reduce-scattered the
+        # moment it is complete, so they are issued immediately
+        self.defer_wgrad = self.world == 1 and bool(
+            cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
+        self._wq = WgradQueue()
+        self.wgrad_rows_reversed = self._blocks_reversed()
         if self.world > 1:
             e = self.shard_buf.element_size()
             gathers = 1 if (self.keep_all or not cfg.reshard_after_forward) else 2
             frac = (self.world - 1) / self.world
             self.comm_bytes_per_step = int(total_sharded * e * frac * (gathers + 1))
+
+    def _slot_key(self, unit, i):
+        """(buffer, element offset) of gradient slot ``i`` of ``unit`` at world size 1."""
+        s = self.p_layout.slots.get((id(unit), i))
+        if s is not None:
+            return 0, s.offset                              # persistent parameters: p_grad
+        g = self._group_of[id(unit)]
+        return 1, g.owner_start + g.layout.slot(unit, i).offset     # owner space (rs_out)
+
+    def _blocks_reversed(self) -> bool:
+        """Whether consecutive blocks' matrix gradients sit at decreasing addresses (the order the
+        model's layer-strided buffers must follow for batched weight gradients)."""
+        blocks = getattr(self.model, "unit_blocks", None) or []
+        if len(blocks) < 2:
+            return False
+        i = next((j for j, shp in enumerate(blocks[0].shapes) if len(shp) == 2), None)
+        if i is None:
+            return False
+        (b0, o0), (b1, o1) = self._slot_key(blocks[0], i), self._slot_key(blocks[1], i)
+        return b0 == b1 and o1 < o0
 
     # ------------------------------------------------------------------ gather / release
     def _launch_gather(self, g):
@@ -250,6 +280,12 @@ class ShardedEngine(Engine):
         if cur < g.total:
             g.grad[cur:g.total].zero_()
 
+    def wgrad(self, unit, i, dy, x, dw, accumulate):
+        if self.defer_wgrad:
+            self._wq.add(unit, i, dy, x, dw, accumulate)
+        else:
+            super().wgrad(unit, i, dy, x, dw, accumulate)
+
     def grads_ready(self, unit):
         g = self._group_of[id(unit)]
         if any(self._persistent(unit, i) for i in range(len(unit.params))):
@@ -292,6 +328,7 @@ class ShardedEngine(Engine):
         # ws == 1: the group gradient buffers ARE the owner gradients; accumulate in place
 
     def _finish_backward(self):
+        self._wq.flush()
         if self._p_left != self._p_pending:      # persistent params of units that never reported
             if self._p_left > 0:
                 self._reduce_persistent()
