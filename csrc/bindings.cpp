@@ -660,6 +660,24 @@ void transpose_into(const Tensor& src, const Tensor& dst) {
   dltb_transpose(src.data_ptr(), dst.data_ptr(), (int)src.size(0), (int)src.size(1), cur_stream());
 }
 
+// batched transpose: nb equally spaced [R, C] matrices starting at src (a 2-D view) -> [C, R] at
+// dst; strides in elements.  The extents are checked against both storages.
+void transpose_batched(const Tensor& src, const Tensor& dst, int64_t nb, int64_t sbs, int64_t dbs) {
+  check_bf16(src, "src");
+  check_bf16(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.is_contiguous() && dst.is_contiguous() &&
+              dst.size(0) == src.size(1) && dst.size(1) == src.size(0), "transpose_batched: shapes");
+  TORCH_CHECK(src.size(1) % 4 == 0 && src.size(0) % 4 == 0 && nb >= 1 && sbs >= 0 && dbs >= 0,
+              "transpose_batched: dims % 4 / batch");
+  TORCH_CHECK(nb == 1 || (sbs >= src.numel() && dbs >= dst.numel()), "transpose_batched: overlapping matrices");
+  const int64_t es = 2;
+  TORCH_CHECK((src.storage_offset() + (nb - 1) * sbs + src.numel()) * es <= (int64_t)src.storage().nbytes() &&
+              (dst.storage_offset() + (nb - 1) * dbs + dst.numel()) * es <= (int64_t)dst.storage().nbytes(),
+              "transpose_batched: batch exceeds the storage");
+  dltb_transpose_batched(src.data_ptr(), dst.data_ptr(), (int)src.size(0), (int)src.size(1), (int)nb,
+                         (long)sbs, (long)dbs, cur_stream());
+}
+
 // ------------------------------------------------------------------------------- GEMM
 // layout "nt": a [M, K], b [N, K] -> out [M, N];  "tn": a [K, M], b [K, N] -> out [M, N]
 // rows may be strided (views of fused buffers); the inner dimension must be contiguous.
@@ -753,6 +771,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_by", &scale_by, py::arg("x"), py::arg("num"), py::arg("den") = py::none(),
         py::arg("g_out") = py::none());
   m.def("transpose_into", &transpose_into);
+  m.def("transpose_batched", &transpose_batched);
   m.def("colreduce_multi", &colreduce_multi);
   m.def("arch", []() { return std::string("gfx950"); });
 }

@@ -11,6 +11,7 @@
 //   f32_from_bf16       dst (+)= float(src)
 //   transpose           dst[C, R] = src[R, C]^T (64x64 LDS tiles; cached W^T for dgrad GEMMs)
 #include "common.h"
+#include "launchers.h"
 
 namespace {
 
@@ -255,8 +256,11 @@ int colsum_splits(int N) {
 // 64x64 tile through LDS (+1 column pad: conflict-free column reads); 256 threads, each moves
 // 16 elements; rows read and written as 8-byte (4 x bf16) vectors along the contiguous dim.
 __global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict__ src,
-                                                       bf16_t* __restrict__ dst, int R, int C) {
+                                                       bf16_t* __restrict__ dst, int R, int C,
+                                                       long sbs, long dbs) {
   __shared__ bf16_t tile[64][65];
+  src += blockIdx.z * sbs;                                     // batch: equally spaced matrices
+  dst += blockIdx.z * dbs;
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;     // 16 x 16 threads, 4 columns each
 #pragma unroll
@@ -384,6 +388,11 @@ void dltb_f32_from_bf16(float* dst, const void* src, long n, int accumulate, hip
 }
 
 void dltb_transpose(const void* src, void* dst, int R, int C, hipStream_t st) {
-  hipLaunchKernelGGL(transpose_kernel, dim3(cdiv(C, 64), cdiv(R, 64)), dim3(256), 0, st,
-                     (const bf16_t*)src, (bf16_t*)dst, R, C);
+  dltb_transpose_batched(src, dst, R, C, 1, 0, 0, st);
+}
+
+void dltb_transpose_batched(const void* src, void* dst, int R, int C, int nb, long sbs, long dbs,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(transpose_kernel, dim3(cdiv(C, 64), cdiv(R, 64), nb), dim3(256), 0, st,
+                     (const bf16_t*)src, (bf16_t*)dst, R, C, sbs, dbs);
 }

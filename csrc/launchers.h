@@ -41,6 +41,9 @@ void dltb_rope(void* qkv, const float* cosb, const float* sinb, int N, int T, in
                int stride, bool inverse, hipStream_t st);
 void dltb_f32_from_bf16(float* dst, const void* src, long n, int accumulate, hipStream_t st);
 void dltb_transpose(const void* src, void* dst, int R, int C, hipStream_t st);
+// nb matrices [R, C] at element stride sbs (src) / dbs (dst) -> [C, R] each, one launch
+void dltb_transpose_batched(const void* src, void* dst, int R, int C, int nb, long sbs, long dbs,
+                            hipStream_t st);
 
 // embedding.hip
 void dltb_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* x, int N, int T,

@@ -111,4 +111,6 @@ class GraphedStep:
          e._window_pos, e._is_boundary, e.last_lr, e._pending_lr, e.opt._lr_now) = s
         e._written.clear()
         e._written.update(written)
+        if hasattr(e, "_wt_epoch"):
+            e._wt_epoch = -1            # transposes "refreshed" inside the failed capture never ran
         e.seed.upload()

@@ -73,7 +73,9 @@ class ReplicatedEngine(Engine):
             self.rs_out = self.acc = None
         del master_full
         self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
-        self._wt_cache = {}      # (unit index, param index) -> (optimizer step, W^T contiguous)
+        self._wt = {}            # (unit index, param index) -> (W view, W^T view of a stacked buffer)
+        self._wt_stack = {}      # (param index, shape) -> [units, K, N] buffer of transposes
+        self._wt_epoch = -1      # optimizer step the cached transposes belong to
         self._ag_pending = {}    # bucket -> async all-gather of updated parameters (deferred step)
         self._defer_opt = (self.stage >= 1 and self.world > 1 and
                            bool(cfg.extra.get("defer_opt", os.environ.get("DLTB_DEFER_OPT", "1") == "1")))
@@ -92,19 +94,45 @@ class ReplicatedEngine(Engine):
 
     # ------------------------------------------------------------------ runtime interface
     def weight_t(self, unit, i, w):
+        """Cached W^T for the NT-form data-gradient GEMM.  The transposes of one parameter kind
+        live in one stacked buffer, row = reversed unit index (the order of the parameters in the
+        flat buffer), so after an optimizer step all of them are refreshed by ONE batched
+        LDS-tiled transpose launch per kind instead of one launch per block."""
         if not self._cache_wt or w.dim() != 2 or not w.is_cuda:
             return None
+        if self._wt_epoch != self.opt_steps:
+            self._refresh_weight_t()
+            self._wt_epoch = self.opt_steps
         key = (unit.index, i)
-        hit = self._wt_cache.get(key)
-        if hit is not None and hit[0] == self.opt_steps:
-            return hit[1]
+        hit = self._wt.get(key)
         if hit is not None:
-            wt = hit[1]
-        else:
-            wt = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
-        ext().transpose_into(w, wt)          # (re-)transpose after an optimizer step (LDS-tiled HIP)
-        self._wt_cache[key] = (self.opt_steps, wt)
+            return hit[1]
+        g = (i, tuple(w.shape))
+        stack = self._wt_stack.get(g)
+        nunits = len(self.model.units())
+        if stack is None:
+            stack = torch.empty((nunits, w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+            self._wt_stack[g] = stack
+        wt = stack[nunits - 1 - unit.index]
+        ext().transpose_into(w, wt)          # first use: transpose now
+        self._wt[key] = (w, wt)
         return wt
+
+    def _refresh_weight_t(self):
+        from .wgrad import strided_batch
+        groups = {}
+        for (uidx, i), (w, wt) in self._wt.items():
+            groups.setdefault((i, tuple(w.shape)), []).append((w, wt))
+        C = ext()
+        for items in groups.values():
+            items.sort(key=lambda it: it[1].data_ptr())
+            W = strided_batch([it[0] for it in items])
+            WT = strided_batch([it[1] for it in items], out=True)
+            if W is not None and WT is not None and len(items) > 1:
+                C.transpose_batched(items[0][0], items[0][1], len(items), W.stride(0), WT.stride(0))
+            else:
+                for w, wt in items:
+                    C.transpose_into(w, wt)
 
     def acquire(self, unit):
         if self._ag_pending:
@@ -217,7 +245,7 @@ class ReplicatedEngine(Engine):
             self._wait_works()
 
     def _after_param_load(self):
-        self._wt_cache.clear()
+        self._wt_epoch = -1                  # cached transposes are stale
         if self.stage >= 1 and self.world > 1:   # other ranks' owner parts
             for bk in self.layout.buckets:
                 full = self.flat_param[bk.start:bk.end]

@@ -420,3 +420,15 @@ def test_sumsq_clip():
     C.clip_coef(acc, 1.0, coef, nrm, 1.0)
     assert abs(nrm.item() - math.sqrt(want)) / math.sqrt(want) < 1e-3
     assert abs(coef.item() - 1.0 / (math.sqrt(want) + 1e-6)) < 1e-6
+
+
+def test_transpose_batched():
+    """nb equally spaced matrices of a flat buffer transposed into a stacked buffer in one launch."""
+    C = ext()
+    R, Cc, nb, gap = 1024, 3072, 5, 4096
+    flat = rnd(nb * (R * Cc + gap))
+    src = [flat[i * (R * Cc + gap):i * (R * Cc + gap) + R * Cc].view(R, Cc) for i in range(nb)]
+    dst = torch.empty(nb, Cc, R, device=DEV, dtype=torch.bfloat16)
+    C.transpose_batched(src[0], dst[0], nb, R * Cc + gap, Cc * R)
+    for i in range(nb):
+        assert torch.equal(dst[i], src[i].t()), i
