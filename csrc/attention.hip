@@ -668,8 +668,34 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
       of[s] = __builtin_bit_cast(bfx8, ld16<uint4>(dorow + 16 * s + 8 * h));
     }
   }
+  float dlt;
+  if (P.o) {   // fused delta = rowsum(dO * O) for this row (replaces attn_bwd_delta_kernel)
+    // summed in attn_bwd_delta_kernel's order (8-element chunks, then its xor butterfly over the
+    // chunks; this lane holds chunks 2s + h), so both paths give bitwise the same delta
+    const bf16_t* orow = P.o + ((long)b * T + qi) * P.o_stride + hq * D;
+    constexpr int NS = D / 16;
+    float cs[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      float a[8], c[8];
+      unpack8(ld16<uint4>(orow + 16 * s + 8 * h), a);
+      unpack8(__builtin_bit_cast(uint4, of[s]), c);
+      float acc = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += c[e] * a[e];
+      cs[s] = acc;
+    }
+#pragma unroll
+    for (int off = NS / 2; off > 0; off >>= 1)
+#pragma unroll
+      for (int s = 0; s < off; ++s) cs[s] += cs[s + off];
+    dlt = cs[0] + __shfl_xor(cs[0], 32, 64);
+    if (sp == 0 && h == 0) const_cast<float*>(P.delta)[bq * T + qi] = dlt;   // read by dK/dV next
+  } else {
+    dlt = P.delta[bq * T + qi];
+  }
   const float nl = -P.lse[bq * T + qi] / P.scale;                                  // S' = S - lse/scale
-  const float nd = -P.delta[bq * T + qi] * (DROP ? 1.f / P.drop_scale : 1.f);     // dP' = dP - delta/s
+  const float nd = -dlt * (DROP ? 1.f / P.drop_scale : 1.f);                       // dP' = dP - delta/s
   const uint32_t* mrow = DROP ? P.mask + ((long)bq * nT * 2 + h) * T + qi : nullptr;
   const float c = P.scale * kLog2e;
   const float nlc = nl * c;
@@ -889,7 +915,7 @@ void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, c
                         const float* lse, const float* delta, const uint32_t* mask, void* out,
                         void* out2, long qs, long ks, long vs, long dos, long outs, long out2s,
                         int B, int T, int Hq, int Hkv, int D, float scale, int causal,
-                        uint32_t thr16, float drop_scale, hipStream_t st) {
+                        uint32_t thr16, float drop_scale, hipStream_t st, const void* o, long os) {
   AttnArgs a = make_args(q, k, v, qs, ks, vs, B, T, Hq, Hkv, scale, causal, thr16, drop_scale,
                          nullptr, 0);
   a.dout = (const bf16_t*)dout;
@@ -901,6 +927,8 @@ void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, c
   a.out_stride = outs;
   a.out2 = (bf16_t*)out2;
   a.out2_stride = out2s;
+  a.o = part == 1 ? (const bf16_t*)o : nullptr;     // dQ pass computes and writes delta itself
+  a.o_stride = os;
   if (part == 0)
     DLTB_ATTN_DISPATCH(launch_dkdv, D, causal != 0, thr16 != 0, a, st);
   else

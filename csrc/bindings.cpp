@@ -461,7 +461,7 @@ Tensor attn_bwd_delta(const Tensor& o, const Tensor& dout, int64_t B, int64_t T,
 void attn_bwd_part(int64_t part, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& dout,
                    const Tensor& lse, const Tensor& delta, const optional<Tensor>& mask,
                    const Tensor& out, const optional<Tensor>& out2, int64_t B, int64_t T, int64_t Hq,
-                   int64_t Hkv, double scale, bool causal, double p) {
+                   int64_t Hkv, double scale, bool causal, double p, const optional<Tensor>& o) {
   const int64_t D = attn_head_dim(q, B, T, Hq);
   check_attn_view(q, "q", B * T, Hq, D);
   check_attn_view(k, "k", B * T, Hkv, D);
@@ -476,6 +476,10 @@ void attn_bwd_part(int64_t part, const Tensor& q, const Tensor& k, const Tensor&
   } else {
     check_attn_view(out, "dq", B * T, Hq, D);
   }
+  if (o.has_value()) {            // dQ pass writes delta = rowsum(dO * O) for the dK/dV pass
+    TORCH_CHECK(part == 1, "attn_bwd_part: o (fused delta) only for the dQ pass");
+    check_attn_view(*o, "o", B * T, Hq, D);
+  }
   const uint32_t thr = thr_of(p);
   const uint32_t* mp = mask_ptr(mask, thr, B, T, Hq);
   dltb_attn_init_attributes();
@@ -484,7 +488,7 @@ void attn_bwd_part(int64_t part, const Tensor& q, const Tensor& k, const Tensor&
                      part == 0 ? out2->data_ptr() : nullptr, q.stride(0), k.stride(0), v.stride(0),
                      dout.stride(0), out.stride(0), part == 0 ? out2->stride(0) : 0, (int)B, (int)T,
                      (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0, thr, scale_of(p),
-                     cur_stream());
+                     cur_stream(), o.has_value() ? o->data_ptr() : nullptr, o.has_value() ? o->stride(0) : 0);
 }
 
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,
@@ -492,8 +496,9 @@ void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o
               const Tensor& dv, int64_t B, int64_t T, int64_t Hq, int64_t Hkv, double scale, bool causal,
               double p) {
   auto delta = attn_bwd_delta(o, dout, B, T, Hq);
-  attn_bwd_part(0, q, k, v, dout, lse, delta, mask, dk, dv, B, T, Hq, Hkv, scale, causal, p);
-  attn_bwd_part(1, q, k, v, dout, lse, delta, mask, dq, c10::nullopt, B, T, Hq, Hkv, scale, causal, p);
+  attn_bwd_part(0, q, k, v, dout, lse, delta, mask, dk, dv, B, T, Hq, Hkv, scale, causal, p, c10::nullopt);
+  attn_bwd_part(1, q, k, v, dout, lse, delta, mask, dq, c10::nullopt, B, T, Hq, Hkv, scale, causal, p,
+                c10::nullopt);
 }
 
 Tensor norm_bwd_dx(const Tensor& dy, const Tensor& s, const Tensor& w, const optional<Tensor>& mean,
@@ -755,7 +760,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("T"), py::arg("Hq"), py::arg("Hkv"), py::arg("scale"), py::arg("causal"), py::arg("p"),
         py::arg("o_out") = py::none());
   m.def("attn_bwd_delta", &attn_bwd_delta);
-  m.def("attn_bwd_part", &attn_bwd_part);
+  m.def("attn_bwd_part", &attn_bwd_part, py::arg("part"), py::arg("q"), py::arg("k"), py::arg("v"),
+        py::arg("dout"), py::arg("lse"), py::arg("delta"), py::arg("mask"), py::arg("out"), py::arg("out2"),
+        py::arg("B"), py::arg("T"), py::arg("Hq"), py::arg("Hkv"), py::arg("scale"), py::arg("causal"),
+        py::arg("p"), py::arg("o") = py::none());
   m.def("attn_bwd", &attn_bwd);
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);

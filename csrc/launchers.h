@@ -91,7 +91,8 @@ void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, c
                         const float* lse, const float* delta, const uint32_t* mask, void* out,
                         void* out2, long qs, long ks, long vs, long dos, long outs, long out2s,
                         int B, int T, int Hq, int Hkv, int D, float scale, int causal,
-                        uint32_t thr16, float drop_scale, hipStream_t st);
+                        uint32_t thr16, float drop_scale, hipStream_t st, const void* o = nullptr,
+                        long os = 0);
 void dltb_attn_init_attributes();
 
 // ---- batched column reductions (colreduce.hip)

@@ -269,13 +269,15 @@ def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal,
     ``par``'s side stream.  Call ``par.join()`` before reading dq."""
     if _gpu(q):
         C = ext()
-        delta = C.attn_bwd_delta(o, do, B, T, Hq)
         m = aux if p > 0 else None
         if par is not None and par.enabled and par.attn:
+            delta = C.attn_bwd_delta(o, do, B, T, Hq)
             with par.fork(q, k, v, do, lse, delta, m):
                 C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p)
         else:
-            C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p)
+            # the dQ pass computes delta = rowsum(dO * O) for its rows and stores it for dK/dV
+            delta = torch.empty_like(lse)
+            C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p, o)
         C.attn_bwd_part(0, q, k, v, do, lse, delta, m, dk, dv, B, T, Hq, Hkv, scale, causal, p)
     else:
         ref.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site)

@@ -362,6 +362,12 @@ def test_attention(B, T, Hq, Hkv, D, causal, p):
     ref.attn_bwd(q, k, v, o, do, lse, *sl(rdqkv), B, T, Hq, Hkv, scale, causal, p, sd, 11)
     for name, a, b in zip("qkv", sl(dqkv), sl(rdqkv)):
         close(a, b, 5e-2, 5e-2, "d" + name)
+    # the model's path: the dQ pass computes delta = rowsum(dO * O) itself (no delta kernel)
+    from dltb.ops import functional as F_
+    fdqkv = torch.empty_like(qkv)
+    F_.attn_bwd(q, k, v, o, do, lse, amask, *sl(fdqkv), B, T, Hq, Hkv, scale, causal, p, sd, 11)
+    for name, a, b in zip("qkv", sl(fdqkv), sl(rdqkv)):
+        close(a, b, 5e-2, 5e-2, "fused-delta d" + name)
 
 
 def test_attention_tinygpt_shape():
