@@ -67,6 +67,8 @@ class TinyGPTBlock(nn.Module):
 # ============================================================================ fused Functions
 # DLTB_MASK_STREAM=1: generate the attention dropout mask on a side stream, concurrent with LN1 + QKV
 _MASK_STREAM = __import__("os").environ.get("DLTB_MASK_STREAM", "0") == "1"
+# DLTB_FUSE_MLP_DROPOUT=0: x2 = x1 + Dropout(m) as its own kernel instead of inside the next LayerNorm
+_FUSE_MLP_DROPOUT = __import__("os").environ.get("DLTB_FUSE_MLP_DROPOUT", "1") == "1"
 
 
 class _EmbedFn(torch.autograd.Function):
@@ -96,18 +98,31 @@ class _EmbedFn(torch.autograd.Function):
 
 
 class _BlockFn(torch.autograd.Function):
+    """One transformer block.  Inputs (x_in, m_in) / outputs (x1, m): a block hands the NEXT
+    consumer its residual x1 and its un-dropped MLP output m, and the consumer's first LayerNorm
+    forms x2 = x1 + Dropout(m) in the same kernel (norm_fwd with a residual; x2 is stored as that
+    LayerNorm's residual stream), so the MLP dropout costs no launch of its own.  Gradient
+    convention between the fused Functions: the consumer returns d(x2) for x1 and None for m; the
+    producing block applies Dropout's backward itself (fused with the fc2 bias column sum)."""
+
     @staticmethod
-    def forward(ctx, x, model, i):
+    def forward(ctx, x_in, m_in, model, i):
+        ctx.set_materialize_grads(False)
         rt, unit = model.rt, model.unit_blocks[i]
         (ln1w, ln1b, win, bin_, wo, bo, ln2w, ln2b, w1, b1, w2, b2) = rt.acquire(unit)
         B, T = model._cur_bt
         cfg = model.cfg
         H, d = cfg.n_head, cfg.n_embd
         p = model.drop_p
-        par = GradStreams(x.device, enabled=_MASK_STREAM or None)
+        par = GradStreams(x_in.device, enabled=_MASK_STREAM or None)
         lb = model.layer_buffer(i)          # layer-strided GEMM operands (batched weight gradients)
-        amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x, par)   # overlaps LN1 + QKV GEMM
-        _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False, y_out=lb and lb.h1)
+        amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x_in, par)   # overlaps LN1 + QKV GEMM
+        if m_in is None:                    # block 0: the embedding output
+            x = x_in
+            _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False, y_out=lb and lb.h1)
+        else:                               # x = x1' + Dropout(m') of the previous block, fused
+            x, h1, mean1, rstd1 = F_.norm_fwd(x_in, m_in, ln1w, ln1b, LN_EPS, False, p, rt.seed,
+                                              model.site_mlp(i - 1), y_out=lb and lb.h1)
         qkv = F_.linear_fwd(h1, win, bin_)
         o, lse, amask = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
                                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i),
@@ -116,15 +131,17 @@ class _BlockFn(torch.autograd.Function):
         x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
         f = F_.linear_fwd(h2, w1, b1)
         g = F_.gelu_fwd(f, out=lb and lb.g)
-        m = F_.linear_fwd(g, w2, b2)
-        x2 = F_.dropout(x1, m, p, rt.seed, model.site_mlp(i))
+        m = F_.linear_fwd(g, w2, b2)        # Dropout(m) + x1 happens in the consumer's LayerNorm
         rt.release_forward(unit)
         ctx.model, ctx.i, ctx.lb = model, i, lb
         ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g)
-        return x2
+        if not _FUSE_MLP_DROPOUT:           # standalone residual + dropout kernel
+            return F_.dropout(x1, m, p, rt.seed, model.site_mlp(i)), None
+        return x1, m
 
     @staticmethod
-    def backward(ctx, dx2):
+    def backward(ctx, dx2, dm_unused):
+        # dx2 = d(x1 + Dropout(m)) from the consumer; m's gradient (Dropout backward) is formed here
         model, i = ctx.model, ctx.i
         rt, unit = model.rt, model.unit_blocks[i]
         (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g) = ctx.saved
@@ -172,16 +189,21 @@ class _BlockFn(torch.autograd.Function):
         par.join()                                            # all of this unit's gradients written
         rt.grads_ready(unit)
         rt.release_backward(unit)
-        return dx, None, None
+        return dx, None, None, None
 
 
 class _HeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, model, targets, return_logits):
+    def forward(ctx, x_in, m_in, model, targets, return_logits):
         rt = model.rt
         lnw, lnb = rt.acquire(model.unit_head)
         wte = rt.acquire_tied(model.unit_embed)[0]
-        _, h, mean, rstd = F_.norm_fwd(x, None, lnw, lnb, LN_EPS, False)
+        if m_in is None:
+            x = x_in
+            _, h, mean, rstd = F_.norm_fwd(x, None, lnw, lnb, LN_EPS, False)
+        else:                               # last block's x1 + Dropout(m), fused into ln_f
+            x, h, mean, rstd = F_.norm_fwd(x_in, m_in, lnw, lnb, LN_EPS, False, model.drop_p, rt.seed,
+                                           model.site_mlp(len(model.unit_blocks) - 1))
         logits = F_.linear_fwd(h, wte)
         if targets is None:
             rt.release_forward(model.unit_head)
@@ -203,7 +225,7 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dlogits_unused, dloss):
         if ctx.no_loss:
-            return None, None, None, None
+            return None, None, None, None, None
         model = ctx.model
         rt = model.rt
         (x, h, mean, rstd, dl, count) = ctx.saved
@@ -221,7 +243,7 @@ class _HeadFn(torch.autograd.Function):
         par.join()
         rt.grads_ready(model.unit_head)
         rt.release_backward(model.unit_head)
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 # ============================================================================ module
@@ -328,9 +350,10 @@ class TinyGPT(nn.Module):
         self._prepare_layer_buffers(B * T, self.transformer["wte"].weight)
         anchor = torch.empty((), requires_grad=True)    # graph entry (CPU scalar, never updated)
         x = _EmbedFn.apply(anchor, idx, self)
+        m = None
         for i in range(len(self.unit_blocks)):
-            x = _BlockFn.apply(x, self, i)
-        logits, loss = _HeadFn.apply(x, self, targets, return_logits)
+            x, m = _BlockFn.apply(x, m, self, i)
+        logits, loss = _HeadFn.apply(x, m, self, targets, return_logits)
         if targets is None:
             return logits.view(B, T, -1), None
         return (logits.view(B, T, -1) if return_logits else None), loss
