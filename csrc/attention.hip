@@ -641,7 +641,15 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
 template <int D>
 constexpr int dq_ks() { return 2; }        // KS = 3 measured neutral at D = 64 (and spills)
 template <int D>
-constexpr int dq_smem_bytes() { return 4 * dq_ks<D>() * kTile * D * 2; }
+constexpr int dq_nst() { return D == 64 ? 3 : 2; }   // LDS ring depth, as the forward's
+template <int D>
+constexpr int dq_stage_bytes() { return 2 * kTile * D * 2 + 1024; }   // K, V, dropout words of 4 waves
+template <int D>
+constexpr int dq_smem_bytes() {
+  constexpr int ring = dq_nst<D>() * dq_ks<D>() * dq_stage_bytes<D>();
+  constexpr int merge = (dq_ks<D>() - 1) * 4 * 16 * (D / 32) * 64 * 4;
+  return ring > merge ? ring : merge;
+}
 
 template <int D, bool CAUSAL, bool DROP, int KS>
 __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
@@ -704,13 +712,25 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
 
+  // NST-deep ring of (K, V, dropout-word) stages per key split, filled by compiler-invisible
+  // LDS-DMA (the forward's scheme): a counted vmcnt retires only the stage about to be read and a
+  // raw s_barrier publishes it, so later stages stay in flight across the barrier.
+  constexpr int NST = dq_nst<D>();
+  constexpr int SB = dq_stage_bytes<D>();
+  constexpr int GL = 2 * GldsTile<D, kTile>::NI + (DROP ? 1 : 0);   // DMA instructions per stage
   const int wv = __builtin_amdgcn_readfirstlane(qw);
-  if (sp < nt) {
-    GldsTile<D, kTile>::load(kbase, P.k_stride, sp * kTile, smem + sp * 2 * TB, wv, lane);
-    GldsTile<D, kTile>::load(vbase, P.v_stride, sp * kTile, smem + sp * 2 * TB + TB, wv, lane);
-  }
-  uint32_t mw_next = (DROP && sp < nt) ? mrow[(long)sp * 2 * T] : 0u;
-  __syncthreads();
+  auto stage_ptr = [&](int it) { return smem + ((it % NST) * KS + sp) * SB; };
+  auto issue = [&](int it) {
+    const int t = it * KS + sp;
+    if (it >= nit || t >= nt) return;
+    char* st = stage_ptr(it);
+    GldsTile<D, kTile, true>::load(kbase, P.k_stride, t * kTile, st, wv, lane);
+    GldsTile<D, kTile, true>::load(vbase, P.v_stride, t * kTile, st + TB, wv, lane);
+    if (DROP) glds4_asm(mrow + (long)t * 2 * T, st + 2 * TB + wv * 256);
+  };
+  wait_vm<0>();        // Q / dO (/ O) fragments and the delta store done: no compiler wait in the loop
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i) issue(i);
 
   f32x16 dq[NACC];
 #pragma unroll
@@ -718,16 +738,14 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
 
   for (int it = 0; it < nit; ++it) {
     const int t = it * KS + sp;
-    const char* kt = smem + ((it & 1) * KS + sp) * 2 * TB;
+    static_assert(NST <= 3, "the counted wait below assumes at most one later stage in flight");
+    if (NST > 2 && it + 1 < nit && (it + 1) * KS + sp < nt) wait_vm<(NST > 2 ? GL : 0)>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    issue(it + NST - 1);                         // refills the buffer read in iteration it - 1
+    const char* kt = stage_ptr(it);
     const char* vt = kt + TB;
-    const uint32_t mw = mw_next;
-    const int tn = t + KS;
-    if (tn < nt) {
-      char* nk = smem + (((it + 1) & 1) * KS + sp) * 2 * TB;
-      GldsTile<D, kTile>::load(kbase, P.k_stride, tn * kTile, nk, wv, lane);
-      GldsTile<D, kTile>::load(vbase, P.v_stride, tn * kTile, nk + TB, wv, lane);
-      if (DROP) mw_next = mrow[(long)tn * 2 * T];
-    }
+    const uint32_t mw = DROP ? *reinterpret_cast<const uint32_t*>(kt + 2 * TB + wv * 256 + lane * 4) : 0u;
     const int kv0 = t * kTile;
     if (t < nt) {
 #pragma unroll
@@ -757,11 +775,11 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
         }
       }
     }
-    __syncthreads();
   }
+  __syncthreads();              // all LDS reads done before the ring is reused for the merge
   if constexpr (KS > 1) {      // splits 1..KS-1 -> LDS -> split 0
     constexpr int NF = 16 * NACC;
-    static_assert((KS - 1) * 4 * NF * 64 * 4 <= 4 * KS * kTile * D * 2, "merge buffer exceeds the LDS ring");
+    static_assert((KS - 1) * 4 * NF * 64 * 4 <= dq_smem_bytes<D>(), "merge buffer exceeds the LDS ring");
     float* red0 = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
     if (sp > 0) {
       float* red = red0 + (sp - 1) * 4 * NF * 64;
