@@ -30,6 +30,7 @@ class FlatAdamW:
         self.step_count = 0
         self._lr_now = float(lr)
         self._tables = None
+        self._seg_blocks = []    # segment -> (first, end) rows of the block tables (contiguous)
         self.hp = None
         if master.is_cuda:
             self._build_tables()
@@ -46,9 +47,11 @@ class FlatAdamW:
             so.append(ostart)
             sl.append(length)
             sd.append(dst.data_ptr())
+            first = len(blk_seg)
             for s in range(ostart, ostart + length, chunk):
                 blk_seg.append(i)
                 blk_start.append(s)
+            self._seg_blocks.append((first, len(blk_seg)))
         dev = self.master.device
         self._tables = (torch.tensor(blk_seg, dtype=torch.int32, device=dev),
                         torch.tensor(blk_start, dtype=torch.int64, device=dev),
@@ -75,6 +78,17 @@ class FlatAdamW:
     def launch(self, grad: torch.Tensor, gscale: torch.Tensor = None):
         b1, b2 = self.betas
         ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, *self._tables, gscale,
+                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp)
+
+    def launch_segment(self, i: int, grad: torch.Tensor, gscale: torch.Tensor = None):
+        """The update of segment ``i`` alone (one launch over a slice of the block tables; the
+        blocks of a segment are contiguous rows).  With ``prepare`` called once per step, the
+        per-segment launches together are exactly ``launch`` -- the engine uses them to let each
+        bucket's forward wait for its own parameters only."""
+        lo, hi = self._seg_blocks[i]
+        b1, b2 = self.betas
+        ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, self._tables[0][lo:hi],
+                    self._tables[1][lo:hi], *self._tables[2:], gscale,
                     self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp)
 
     @torch.no_grad()

@@ -9,13 +9,15 @@ from dltb.parallel import GraphedStep, engine_config, make_engine
 pytestmark = pytest.mark.gpu
 
 
-def _run(strategy, graphed, tier="A", T=256, layers=2, windows=4):
+def _run(strategy, graphed, tier="A", T=256, layers=2, windows=4, extra=None):
     torch.manual_seed(0)
     cfg = get_model_config(tier, T)
     cfg.n_layer = layers
     with torch.device("cuda"):
         model = build_model(cfg)
-    eng = make_engine(model, engine_config(strategy, 4, "reference"), "cuda:0")
+    ecfg = engine_config(strategy, 4, "reference")
+    ecfg.extra.update(extra or {})
+    eng = make_engine(model, ecfg, "cuda:0")
     eng.train()
     g = torch.Generator(device="cuda").manual_seed(1)
     runner = GraphedStep(eng) if graphed else None
@@ -54,5 +56,16 @@ def test_graph_replay_mistral():
     l0, s0 = _run("zero3", False, tier="mtiny", layers=2)
     l1, s1 = _run("zero3", True, tier="mtiny", layers=2)
     assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_overlapped_optimizer_matches_in_order(graphed):
+    """World-1 ZeRO-2 runs the window's AdamW on a side stream, per bucket, overlapping the next
+    forward: the same kernels on the same data, so training is bitwise the in-order step."""
+    l0, s0 = _run("zero2", graphed, extra={"overlap_opt": False})
+    l1, s1 = _run("zero2", graphed, extra={"overlap_opt": True})
+    assert l0 == l1, (l0, l1)
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
