@@ -190,13 +190,13 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
 }
 
 template <int D>
-constexpr int fwd_ks() { return D == 64 ? 3 : 2; }   // KS = 4 at D = 64 spills (128 VGPRs) and is slower
-template <int D>
-constexpr int fwd_nst() { return D == 64 ? 3 : 2; }  // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
+constexpr int fwd_ks() { return D == 64 ? 3 : 2; }   // KS = 4 (2-deep ring, 128 VGPRs) measured 2 % faster: not worth the spill risk
+template <int D, int KS>
+constexpr int fwd_nst() { return D == 64 && KS < 4 ? 3 : 2; }  // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
 template <int D>
 constexpr int fwd_stage_bytes() { return 2 * kTile * D * 2 + 1024; }   // K, V, dropout words of 4 waves
-template <int D>
-constexpr int fwd_smem_bytes() { return fwd_nst<D>() * fwd_ks<D>() * fwd_stage_bytes<D>(); }
+template <int D, int KS = fwd_ks<D>()>
+constexpr int fwd_smem_bytes() { return fwd_nst<D, KS>() * KS * fwd_stage_bytes<D>(); }
 
 template <int D, bool CAUSAL, bool DROP, int KS>
 __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
@@ -223,24 +223,31 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   const int nit = (nt + KS - 1) / KS;
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
-  const uint32_t* mrow = DROP ? P.mask + ((long)bh * nT * 2 + h) * T + qi : nullptr;
+  const uint32_t* mbase = DROP ? P.mask + (long)bh * nT * 2 * T : nullptr;   // wave-uniform
+  const uint32_t* mrow = DROP ? mbase + (long)h * T + qi : nullptr;
   const float c = P.scale * kLog2e;
 
   // NST-deep ring of (K, V, dropout-word) stages per key split, filled by compiler-invisible
   // LDS-DMA; a counted vmcnt retires only the stage about to be read and a raw s_barrier
   // publishes it, so NST-2 later stages stay in flight across the barrier.
-  constexpr int NST = fwd_nst<D>();
+  constexpr int NST = fwd_nst<D, KS>();
   constexpr int SB = fwd_stage_bytes<D>();
   constexpr int GL = 2 * GldsTile<D, kTile>::NI + (DROP ? 1 : 0);   // DMA instructions per stage
   const int wv = __builtin_amdgcn_readfirstlane(qw);
   auto stage_ptr = [&](int it) { return smem + ((it % NST) * KS + sp) * SB; };
+  // per-lane DMA offsets are tile-invariant; the tile's row goes into the SGPR base (SALU only)
+  uint32_t koff[GldsTile<D, kTile>::NI], voff[GldsTile<D, kTile>::NI];
+  GldsTile<D, kTile>::offsets(P.k_stride, wv, lane, koff);
+  GldsTile<D, kTile>::offsets(P.v_stride, wv, lane, voff);
+  const uint32_t moff = (uint32_t)(mrow - mbase) * 4u;
+  const int spu = __builtin_amdgcn_readfirstlane(sp);      // the key split is wave-uniform
   auto issue = [&](int it) {
-    const int t = it * KS + sp;
+    const int t = it * KS + spu;
     if (it >= nit || t >= nt) return;
-    char* st = stage_ptr(it);
-    GldsTile<D, kTile, true>::load(kbase, P.k_stride, t * kTile, st, wv, lane);
-    GldsTile<D, kTile, true>::load(vbase, P.v_stride, t * kTile, st + TB, wv, lane);
-    if (DROP) glds4_asm(mrow + (long)t * 2 * T, st + 2 * TB + wv * 256);
+    char* st = smem + ((it % NST) * KS + spu) * SB;
+    GldsTile<D, kTile>::load_sv(kbase + (long)t * kTile * P.k_stride, koff, st, wv);
+    GldsTile<D, kTile>::load_sv(vbase + (long)t * kTile * P.v_stride, voff, st + TB, wv);
+    if (DROP) glds4_sv(mbase + (long)t * 2 * T, moff, st + 2 * TB + wv * 256);
   };
   wait_vm<0>();        // Q fragments landed: no compiler vmcnt wait for them inside the loop
 #pragma unroll
@@ -292,14 +299,19 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
 #pragma unroll
         for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
       }
-      float ls = 0.f;
-      static_for<32>([&](auto I) {
-        constexpr int n = I / 16, i = I % 16;
-        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[n][i], c, -m));
-        ls += p;
-        sacc[n][i] = DROP ? keep_and<I>(p, mw) : p;
+      // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two probabilities per VALU op
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 c2 = {c, c}, nm2 = {-m, -m};
+      f32x2 ls2 = {0.f, 0.f};
+      static_for<16>([&](auto J) {
+        constexpr int n = J / 8, i = 2 * (J % 8);
+        const f32x2 x = __builtin_elementwise_fma(f32x2{sacc[n][i], sacc[n][i + 1]}, c2, nm2);
+        const f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+        ls2 += p;
+        sacc[n][i] = DROP ? keep_and<16 * n + i>(p[0], mw) : p[0];
+        sacc[n][i + 1] = DROP ? keep_and<16 * n + i + 1>(p[1], mw) : p[1];
       });
-      l += ls;
+      l += ls2[0] + ls2[1];
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
 #pragma unroll
@@ -549,19 +561,31 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
         }
         const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
         const uint32_t Mv[4] = {M4.x, M4.y, M4.z, M4.w};
+        // packed fp32 (v_pk_mul / v_pk_add): two scores per VALU op, same roundings
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 c2 = {c, c};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < 4; e += 2) {
           const int i = 4 * g4 + e;
-          float p = __builtin_amdgcn_exp2f(sa[i] * c);
-          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
+          const f32x2 x = f32x2{sa[i], sa[i + 1]} * c2;
+          f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p[0] = 0.f;
+          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e + 1) p[1] = 0.f;
+          f32x2 d;
           if (DROP) {
-            const uint32_t km = keep_mask_v(Mv[e], jbit);
-            pd[i] = __uint_as_float(__float_as_uint(p) & km);
-            ds[i] = p * (__uint_as_float(__float_as_uint(dp[i]) & km) + Dv[e]);
+            const uint32_t k0m = keep_mask_v(Mv[e], jbit), k1m = keep_mask_v(Mv[e + 1], jbit);
+            pd[i] = __uint_as_float(__float_as_uint(p[0]) & k0m);
+            pd[i + 1] = __uint_as_float(__float_as_uint(p[1]) & k1m);
+            const f32x2 dd = f32x2{__uint_as_float(__float_as_uint(dp[i]) & k0m),
+                                   __uint_as_float(__float_as_uint(dp[i + 1]) & k1m)} + f32x2{Dv[e], Dv[e + 1]};
+            d = p * dd;
           } else {
-            pd[i] = p;
-            ds[i] = p * dp[i];
+            pd[i] = p[0];
+            pd[i + 1] = p[1];
+            d = p * f32x2{dp[i], dp[i + 1]};
           }
+          ds[i] = d[0];
+          ds[i + 1] = d[1];
         }
       }
     };
@@ -704,7 +728,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
   }
   const float nl = -P.lse[bq * T + qi] / P.scale;                                  // S' = S - lse/scale
   const float nd = -dlt * (DROP ? 1.f / P.drop_scale : 1.f);                       // dP' = dP - delta/s
-  const uint32_t* mrow = DROP ? P.mask + ((long)bq * nT * 2 + h) * T + qi : nullptr;
+  const uint32_t* mbase = DROP ? P.mask + (long)bq * nT * 2 * T : nullptr;   // wave-uniform
+  const uint32_t* mrow = DROP ? mbase + (long)h * T + qi : nullptr;
   const float c = P.scale * kLog2e;
   const float nlc = nl * c;
   const int nt = CAUSAL ? min(nT, (qb * kBlockRows + kBlockRows - 1) / kTile + 1) : nT;
@@ -720,13 +745,19 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
   constexpr int GL = 2 * GldsTile<D, kTile>::NI + (DROP ? 1 : 0);   // DMA instructions per stage
   const int wv = __builtin_amdgcn_readfirstlane(qw);
   auto stage_ptr = [&](int it) { return smem + ((it % NST) * KS + sp) * SB; };
+  // per-lane DMA offsets are tile-invariant; the tile's row goes into the SGPR base (SALU only)
+  uint32_t koff[GldsTile<D, kTile>::NI], voff[GldsTile<D, kTile>::NI];
+  GldsTile<D, kTile>::offsets(P.k_stride, wv, lane, koff);
+  GldsTile<D, kTile>::offsets(P.v_stride, wv, lane, voff);
+  const uint32_t moff = (uint32_t)(mrow - mbase) * 4u;
+  const int spu = __builtin_amdgcn_readfirstlane(sp);      // the key split is wave-uniform
   auto issue = [&](int it) {
-    const int t = it * KS + sp;
+    const int t = it * KS + spu;
     if (it >= nit || t >= nt) return;
-    char* st = stage_ptr(it);
-    GldsTile<D, kTile, true>::load(kbase, P.k_stride, t * kTile, st, wv, lane);
-    GldsTile<D, kTile, true>::load(vbase, P.v_stride, t * kTile, st + TB, wv, lane);
-    if (DROP) glds4_asm(mrow + (long)t * 2 * T, st + 2 * TB + wv * 256);
+    char* st = smem + ((it % NST) * KS + spu) * SB;
+    GldsTile<D, kTile>::load_sv(kbase + (long)t * kTile * P.k_stride, koff, st, wv);
+    GldsTile<D, kTile>::load_sv(vbase + (long)t * kTile * P.v_stride, voff, st + TB, wv);
+    if (DROP) glds4_sv(mbase + (long)t * 2 * T, moff, st + 2 * TB + wv * 256);
   };
   wait_vm<0>();        // Q / dO (/ O) fragments and the delta store done: no compiler wait in the loop
 #pragma unroll
@@ -759,12 +790,21 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
         }
         const bool diag = CAUSAL && kv0 + 32 * n + 31 > q0;
         f32x16 ds;
-        static_for<16>([&](auto I) {
-          constexpr int i = I;
-          float p = __builtin_amdgcn_exp2f(fmaf(sa[i], c, nlc));
-          if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
-          const float dpv = DROP ? (n == 0 ? keep_and<I>(dp[i], mw) : keep_and<16 + I>(dp[i], mw)) : dp[i];
-          ds[i] = p * (dpv + nd);
+        // packed fp32 (v_pk_fma / v_pk_add / v_pk_mul): two scores per VALU op, same roundings
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 c2 = {c, c}, nl2 = {nlc, nlc}, nd2 = {nd, nd};
+        static_for<8>([&](auto J) {
+          constexpr int i = 2 * J;
+          const f32x2 x = __builtin_elementwise_fma(f32x2{sa[i], sa[i + 1]}, c2, nl2);
+          f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+          if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p[0] = 0.f;
+          if (diag && kv0 + 32 * n + ((i + 1) & 3) + 8 * ((i + 1) >> 2) + 4 * h > qi) p[1] = 0.f;
+          const f32x2 dpv = DROP ? (n == 0 ? f32x2{keep_and<i>(dp[i], mw), keep_and<i + 1>(dp[i + 1], mw)}
+                                           : f32x2{keep_and<16 + i>(dp[i], mw), keep_and<17 + i>(dp[i + 1], mw)})
+                                 : f32x2{dp[i], dp[i + 1]};
+          const f32x2 d = p * (dpv + nd2);
+          ds[i] = d[0];
+          ds[i + 1] = d[1];
         });
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {

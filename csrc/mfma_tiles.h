@@ -85,6 +85,34 @@ DLTB_DEV void glds4_asm(const void* gsrc, const void* lds_dst) {
                : "memory");
 }
 
+// Scalar-base forms: address = wave-uniform 64-bit base (SGPR pair, advanced per tile by SALU) +
+// a loop-invariant per-lane 32-bit byte offset (VGPR) -- no per-tile VALU address arithmetic.
+DLTB_DEV uint64_t uniform_ptr(const void* p) {
+  const uint64_t b = (uint64_t)(uintptr_t)p;
+  // (readfirstlane returns int: widen through uint32_t, never sign-extend the low half)
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  return ((uint64_t)hi << 32) | (uint64_t)lo;
+}
+DLTB_DEV void glds16_sv(const void* sbase, uint32_t voff, const void* lds_dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds)
+               : "memory");
+}
+DLTB_DEV void glds4_sv(const void* sbase, uint32_t voff, const void* lds_dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(uniform_ptr(sbase)), "s"(lds)
+               : "memory");
+}
+
 // s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14, expcnt / lgkmcnt at max)
 template <int N>
 DLTB_DEV void wait_vm() {
@@ -110,6 +138,20 @@ struct GldsTile {
                                          (__attribute__((address_space(3))) void*)(tile + (wv * NI + i) * 1024),
                                          16, 0, 0);
     }
+  }
+  // per-lane byte offsets of the NI DMA instructions relative to row row0 (tile-invariant)
+  DLTB_DEV static void offsets(long stride, int wv, int lane, uint32_t (&off)[NI]) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int lin = (wv * NI + i) * 64 + lane;
+      const int row = lin / CH, pos = lin % CH;
+      off[i] = (uint32_t)((row * stride + ((pos ^ swz<D>(row)) << 3)) * 2);
+    }
+  }
+  // rows row0 .. row0 + ROWS - 1 with row0 folded into the (wave-uniform) base pointer
+  DLTB_DEV static void load_sv(const bf16_t* base_row0, const uint32_t (&off)[NI], char* tile, int wv) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) glds16_sv(base_row0, off[i], tile + (wv * NI + i) * 1024);
   }
 };
 
