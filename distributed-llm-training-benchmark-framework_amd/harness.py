@@ -36,6 +36,7 @@ from .results import make_record, print_markers, print_result, write_result
 from .utils.dist import all_reduce_max, barrier, cleanup_distributed, resolve_ranks, setup_distributed
 from .utils.gemm_tuning import flush_tunableop, setup_tunableop
 from .utils.platform import MI355X_DENSE_BF16_FLOPS, device_info
+from .utils.timers import PhaseTimers
 
 DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
 
@@ -73,6 +74,9 @@ def build_parser():
     p.add_argument("--data-loader", choices=["device", "host"], default="device")
     p.add_argument("--profile", type=str, default=None, help="write a torch.profiler chrome trace to this dir")
     p.add_argument("--profile-steps", type=int, default=3)
+    p.add_argument("--phase-timers", action="store_true",
+                   help="per-phase times (forward / backward / exposed comm wait / optimizer) from HIP events; "
+                        "runs eagerly (a graph replay has no phase boundaries)")
     p.add_argument("--debug-collectives", action="store_true", help="TORCH_DISTRIBUTED_DEBUG=DETAIL")
     p.add_argument("--fail-at-step", type=int, default=None, help="inject a failure (tests the suite runner)")
     p.add_argument("--timeout-min", type=int, default=30, help="collective timeout")
@@ -147,7 +151,9 @@ def train(args):
             if is_main:
                 print(f"Resumed from {args.resume}: optimizer step {meta['opt_steps']}", flush=True)
         engine.train()
-        runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device, world) and not args.profile) else None
+        runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device, world) and not args.profile
+                                         and not args.phase_timers) else None
+        timers = PhaseTimers(device) if args.phase_timers else None
         losses = []
         step_events = []
         host_times = []
@@ -174,12 +180,23 @@ def train(args):
                 ev1 = torch.cuda.Event(enable_timing=True)
                 ev0.record()
             h0 = time.perf_counter()
+            timed_phase = timers is not None and step >= args.warmup_steps
+            if timed_phase:
+                engine.timers = timers
+                timers.begin_step()
             if runner is not None:
                 loss = runner(batch, targets)
             else:
                 loss = engine(batch, targets)[1]
+                if timed_phase:
+                    timers.mark("fwd_end")
                 engine.backward(loss)
+                if timed_phase:
+                    timers.mark("bwd_end")
                 engine.step()
+            if timed_phase:
+                timers.end_step()
+                engine.timers = None
             h1 = time.perf_counter()
             if ev1 is not None:
                 ev1.record()
@@ -246,6 +263,7 @@ def train(args):
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
             "accum_semantics": args.accum_semantics, "dtype": args.dtype, "data_loader": args.data_loader,
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
+            "phase_times_ms": timers.summary() if timers is not None else None,
         }
         if is_main:
             print_result(record)

@@ -76,8 +76,13 @@ class Engine(ParamRuntime):
         self._norm_sq = torch.zeros(1, device=self.device, dtype=torch.float32)
         self._gscale = torch.ones(1, device=self.device, dtype=torch.float32)
         self.comm_bytes_per_step = 0
+        self.timers = None               # utils.timers.PhaseTimers while the harness times phases
         model.rt = self
         self._setup()
+
+    def _phase(self, name: str):
+        if self.timers is not None:
+            self.timers.mark(name)
 
     # ------------------------------------------------------------------ subclass hooks
     def _setup(self):
@@ -127,7 +132,9 @@ class Engine(ParamRuntime):
     def _run_pending_opt(self):
         if self._pending_lr is not None:
             lr, self._pending_lr = self._pending_lr, None
+            self._phase("opt_begin")
             self._deferred_optimizer_step(lr)
+            self._phase("opt_end")
 
     def _deferred_optimizer_step(self, lr: float):
         self._optimizer_step(lr)

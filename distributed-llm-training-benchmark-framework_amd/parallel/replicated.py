@@ -214,7 +214,9 @@ class ReplicatedEngine(Engine):
             for b, done in enumerate(self._launched):   # units that never reported (unused params)
                 if not done:
                     self._launch(b)
+        self._phase("comm_wait_begin")
         self._wait_works()
+        self._phase("comm_wait_end")
         self._pending = [len(b.units) for b in self.layout.buckets]
         self._launched = [False] * len(self.layout.buckets)
         if self.stage == 2 and self.acc is not None:

@@ -336,7 +336,9 @@ class ShardedEngine(Engine):
         for g in self.groups:                     # groups whose backward did not run fully
             self._reduce_group(g)
             g.bwd_left = len(g.units)
+        self._phase("comm_wait_begin")
         self._wait_works()
+        self._phase("comm_wait_end")
         self._held_grads.clear()
         if self.acc is not None:
             first = self._window_pos == 0

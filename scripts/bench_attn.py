@@ -19,6 +19,7 @@ import dltb  # noqa: E402,F401
 from dltb.ops._ext import ext  # noqa: E402
 
 SHAPES = {"tinygpt_a": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.1),
+          "tinygpt_a_p0": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.0),
           "m7b": dict(B=1, T=4096, Hq=32, Hkv=8, D=128, causal=True, p=0.0)}
 
 
