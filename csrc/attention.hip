@@ -574,11 +574,13 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
           f32x2 d;
           if (DROP) {
             const uint32_t k0m = keep_mask_v(Mv[e], jbit), k1m = keep_mask_v(Mv[e + 1], jbit);
-            pd[i] = __uint_as_float(__float_as_uint(p[0]) & k0m);
-            pd[i + 1] = __uint_as_float(__float_as_uint(p[1]) & k1m);
-            const f32x2 dd = f32x2{__uint_as_float(__float_as_uint(dp[i]) & k0m),
-                                   __uint_as_float(__float_as_uint(dp[i + 1]) & k1m)} + f32x2{Dv[e], Dv[e + 1]};
-            d = p * dd;
+            // dS = p (keep dP' + D) = fma(p keep, dP', p D): the masked probability (needed for dV
+            // anyway) carries the keep bit, so dP' needs no mask of its own
+            const f32x2 pdv = {__uint_as_float(__float_as_uint(p[0]) & k0m),
+                               __uint_as_float(__float_as_uint(p[1]) & k1m)};
+            pd[i] = pdv[0];
+            pd[i + 1] = pdv[1];
+            d = __builtin_elementwise_fma(pdv, f32x2{dp[i], dp[i + 1]}, p * f32x2{Dv[e], Dv[e + 1]});
           } else {
             pd[i] = p[0];
             pd[i + 1] = p[1];

@@ -52,6 +52,13 @@ def setup_distributed(world_size, rank, local_rank, master_addr=None, master_por
                   timeout=datetime.timedelta(minutes=timeout_min))
         if device_type == "cuda":
             kw["device_id"] = device
+            if os.environ.get("DLTB_COMM_HIGH_PRIORITY", "1") == "1":
+                # RCCL's internal stream at high priority: when bucket collectives and backward
+                # kernels are both queued, the dispatcher places the collective's workgroups first,
+                # so the reduce-scatter / all-gather progresses under the compute instead of behind it
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
         dist.init_process_group(**kw)
         if device_type == "cuda":      # warm the communicator up outside the timed region
             t = torch.ones(1, device=device)
