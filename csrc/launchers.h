@@ -98,7 +98,7 @@ void dltb_attn_init_attributes();
 // ---- batched column reductions (colreduce.hip)
 enum { DLTB_COLPART_PLAIN = 0, DLTB_COLPART_GELU = 1, DLTB_COLPART_DROP = 2, DLTB_COLPART_LN = 3,
        DLTB_COLPART_RMS = 4 };
-#define DLTB_COLRED_MAX 12
+#define DLTB_COLRED_MAX 64   // segments per colreduce_multi launch (kernel-argument struct: 2 KiB)
 struct DltbColPartSeg {
   const uint16_t* a;
   const uint16_t* b;

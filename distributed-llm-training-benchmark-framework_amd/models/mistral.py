@@ -134,7 +134,8 @@ class _LayerFn(torch.autograd.Function):
         dgu = F_.swiglu_bwd(dhh, gu)
         F_.linear_wgrad(dgu, h2, s[4][0], None, s[4][1])
         dh2 = F_.linear_dgrad(dgu, wgu, rt.weight_t(unit, 4, wgu))
-        red = F_.GradReducer()
+        shared = rt.grad_reducer()
+        red = shared if shared is not None else F_.GradReducer()
         dx1 = F_.norm_bwd(dh2, x1, w_post, None, rstd2, dx2, s[3][0], None, s[3][1], True, red=red)
         F_.linear_wgrad(dx1, o, s[2][0], None, s[2][1])
         do = F_.linear_dgrad(dx1, wo, rt.weight_t(unit, 2, wo))
@@ -147,7 +148,8 @@ class _LayerFn(torch.autograd.Function):
         F_.linear_wgrad(dqkv, h1, s[1][0], None, s[1][1])
         dh1 = F_.linear_dgrad(dqkv, wqkv, rt.weight_t(unit, 1, wqkv))
         dx = F_.norm_bwd(dh1, x, w_in, None, rstd1, dx1, s[0][0], None, s[0][1], True, red=red)
-        red.flush()
+        if shared is None:
+            red.flush()
         rt.grads_ready(unit)
         rt.release_backward(unit)
         return dx, None, None

@@ -162,7 +162,10 @@ class _BlockFn(torch.autograd.Function):
             else:
                 rt.wgrad(unit, j, dy, xin, s[j][0], s[j][1])
 
-        red = F_.GradReducer()   # the 8 bias / LayerNorm column sums: fused partials, ONE reduce launch
+        # the 8 bias / LayerNorm column sums: fused partials, reduced by ONE launch per block (or,
+        # with the engine's shared reducer at world size 1, one launch for all blocks)
+        shared = rt.grad_reducer()
+        red = shared if shared is not None else F_.GradReducer()
         # MLP
         dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
                                  out=lb and lb.dm)
@@ -185,7 +188,8 @@ class _BlockFn(torch.autograd.Function):
         dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False, par,
                          red, bias=(dqkv, s[3][0], s[3][1]))
-        red.flush()
+        if shared is None:
+            red.flush()
         par.join()                                            # all of this unit's gradients written
         rt.grads_ready(unit)
         rt.release_backward(unit)

@@ -52,15 +52,16 @@ class GradReducer:
     gradient slot with ONE ``colreduce_multi`` launch (instead of one reduce launch per bias /
     norm weight).  On the CPU the ops reduce immediately and this is a no-op."""
 
-    MAX = 12
+    MAX = 64                     # csrc/launchers.h DLTB_COLRED_MAX
 
-    def __init__(self):
+    def __init__(self, max_sets: int = 12):
+        self.max_sets = min(int(max_sets), self.MAX)
         self.parts, self.outs, self.acc = [], [], []
 
     def add(self, part2d, out, accumulate):
         if out is None:
             return
-        if len(self.parts) == self.MAX:
+        if len(self.parts) == self.max_sets:
             self.flush()
         self.parts.append(part2d)
         self.outs.append(out)

@@ -23,6 +23,7 @@ import os
 
 import torch
 
+from ..ops import functional as F_
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
 from .engine import Engine
@@ -100,6 +101,11 @@ class ReplicatedEngine(Engine):
         # flushes once per backward, world > 1 per bucket right before its collective
         self.defer_wgrad = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
         self._wq = WgradQueue()
+        # world 1: nothing reads a gradient slot before the backward ends, so the bias / norm-weight
+        # column sums of ALL blocks are reduced by one or two colreduce_multi launches at its end
+        # instead of one launch per block
+        self._red = F_.GradReducer(64) if (self.world == 1 and dev.type == "cuda" and bool(
+            cfg.extra.get("shared_colreduce", os.environ.get("DLTB_SHARED_COLREDUCE", "1") == "1"))) else None
         self._launched = [False] * len(L.buckets)
         nbytes = L.total * elem
         if self.world > 1:
@@ -182,6 +188,9 @@ class ReplicatedEngine(Engine):
         else:
             super().wgrad(unit, i, dy, x, dw, accumulate)
 
+    def grad_reducer(self):
+        return self._red
+
     def grads_ready(self, unit):
         b = self._bucket_of.get(id(unit))
         if b is None:
@@ -209,6 +218,8 @@ class ReplicatedEngine(Engine):
 
     def _finish_backward(self):
         self._join_opt_stream()
+        if self._red is not None:
+            self._red.flush()
         self._wq.flush()                                        # world 1: every block in one batch
         if self._reduce_now():
             for b, done in enumerate(self._launched):   # units that never reported (unused params)

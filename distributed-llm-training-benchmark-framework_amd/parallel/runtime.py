@@ -88,6 +88,12 @@ class ParamRuntime:
     # (backward-ordered replicated layouts); the model's layer-strided buffers follow it
     wgrad_rows_reversed = True
 
+    def grad_reducer(self):
+        """A column-sum reducer shared by every block's backward (flushed by the engine once per
+        backward), or None: each block reduces its own bias / norm-weight sums before it reports
+        its gradients (``grads_ready``)."""
+        return None
+
     def wgrad(self, unit: Unit, i: int, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor,
               accumulate: bool):
         """Write ``dy^T x`` into gradient slot ``dw`` (``accumulate``: add).  The default issues it

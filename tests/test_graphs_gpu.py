@@ -69,3 +69,13 @@ def test_overlapped_optimizer_matches_in_order(graphed):
     assert l0 == l1, (l0, l1)
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+def test_shared_column_reducer_matches_per_block():
+    """World 1: the bias / norm-weight column sums of all blocks reduced at the end of the backward
+    (one colreduce_multi launch for up to 64 sums) equal the per-block reduction bitwise."""
+    l0, s0 = _run("zero2", True, extra={"shared_colreduce": False})
+    l1, s1 = _run("zero2", True, extra={"shared_colreduce": True})
+    assert l0 == l1, (l0, l1)
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
