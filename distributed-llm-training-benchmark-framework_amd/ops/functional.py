@@ -54,9 +54,17 @@ class GradReducer:
 
     MAX = 64                     # csrc/launchers.h DLTB_COLRED_MAX
 
-    def __init__(self, max_sets: int = 12):
+    def __init__(self, max_sets: int = 12, defer_plain: bool = False):
         self.max_sets = min(int(max_sets), self.MAX)
         self.parts, self.outs, self.acc = [], [], []
+        # plain column sums whose partials may ride along with the NEXT colpart launch (the
+        # engine's shared reducer: the QKV bias sum of block i joins block i-1's dropout colpart)
+        self.defer_plain = bool(defer_plain)
+        self.pending = []
+
+    def take_pending(self, n: int):
+        out, self.pending = self.pending[:n], self.pending[n:]
+        return out
 
     def add(self, part2d, out, accumulate):
         if out is None:
@@ -68,6 +76,13 @@ class GradReducer:
         self.acc.append(bool(accumulate))
 
     def flush(self):
+        while self.pending:
+            extra = self.take_pending(3)
+            parts = ext().colpart([_PLAIN] * len(extra), [e[0] for e in extra], [None] * len(extra),
+                                  [None] * len(extra), [None] * len(extra), [None] * len(extra), 0.0, None,
+                                  [0] * len(extra))
+            for (src, out, acc), pt in zip(extra, parts):
+                self.add(pt[0], out, acc)
         if self.parts:
             ext().colreduce_multi(self.parts, self.outs, self.acc)
             self.parts, self.outs, self.acc = [], [], []
@@ -92,6 +107,8 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
                 red.add(part[1], gb, accumulate)
             if dx_sum:
                 red.add(part[-1], bias[1], bias[2])
+            elif has_bias and red.defer_plain:
+                red.pending.append((bias[0], bias[1], bias[2]))
             elif has_bias:
                 parts = C.colpart([_PLAIN], [bias[0]], [None], [None], [None], [None], 0.0, None, [0])
                 red.add(parts[0][0], bias[1], bias[2])
@@ -146,8 +163,17 @@ def dropout_bwd_bias(g, p, seed, site, db, accumulate, red, out=None):
     """dm = dropout_mask(g) / (1-p) (the Dropout backward) with colsum(dm) -> db fused."""
     if _gpu(g):
         dm = torch.empty_like(g) if out is None else out
-        parts = ext().colpart([_DROP], [g], [None], [dm], [None], [None], p, _sd(seed) if p > 0 else None, [site])
+        rows, keep, extra = g.numel() // g.shape[-1], [], []
+        for e in red.pending:               # colpart segments must share the row count
+            (extra if len(extra) < 2 and e[0].numel() // e[0].shape[-1] == rows else keep).append(e)
+        red.pending = keep
+        n = len(extra)
+        parts = ext().colpart([_DROP] + [_PLAIN] * n, [g] + [e[0] for e in extra], [None] * (n + 1),
+                              [dm] + [None] * n, [None] * (n + 1), [None] * (n + 1), p,
+                              _sd(seed) if p > 0 else None, [site] + [0] * n)
         red.add(parts[0][0], db, accumulate)
+        for (src, o, acc), pt in zip(extra, parts[1:]):
+            red.add(pt[0], o, acc)
         return dm
     dm = _into(out, ref.dropout(None, g, p, seed, site))
     if db is not None:

@@ -103,8 +103,9 @@ class ReplicatedEngine(Engine):
         self._wq = WgradQueue()
         # world 1: nothing reads a gradient slot before the backward ends, so the bias / norm-weight
         # column sums of ALL blocks are reduced by one or two colreduce_multi launches at its end
-        # instead of one launch per block
-        self._red = F_.GradReducer(64) if (self.world == 1 and dev.type == "cuda" and bool(
+        # instead of one launch per block, and the QKV-bias partials of block i ride along with
+        # block i-1's dropout colpart launch instead of a launch of their own
+        self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda" and bool(
             cfg.extra.get("shared_colreduce", os.environ.get("DLTB_SHARED_COLREDUCE", "1") == "1"))) else None
         self._launched = [False] * len(L.buckets)
         nbytes = L.total * elem
