@@ -525,7 +525,8 @@ Tensor norm_bwd_dx(const Tensor& dy, const Tensor& s, const Tensor& w, const opt
 std::tuple<Tensor, Tensor> norm_bwd_fused(const Tensor& dy, const Tensor& s, const Tensor& w,
                                           const optional<Tensor>& mean, const Tensor& rstd,
                                           const optional<Tensor>& dres, bool rms, bool dx_sum,
-                                          const optional<Tensor>& dx_out) {
+                                          const optional<Tensor>& dx_out, const optional<Tensor>& dm_out,
+                                          double drop_p, const optional<Tensor>& seed, int64_t site) {
   check_contig_bf16(dy, "dy");
   check_contig_bf16(s, "s");
   check_contig_bf16(w, "w");
@@ -539,11 +540,19 @@ std::tuple<Tensor, Tensor> norm_bwd_fused(const Tensor& dy, const Tensor& s, con
     TORCH_CHECK(dres->sizes() == dy.sizes(), "norm_bwd_fused: dres shape");
   }
   auto dx = out_or_new(dx_out, dy, "norm_bwd_fused dx_out");
-  const int64_t K = (rms ? 1 : 2) + (dx_sum ? 1 : 0);
+  void* dm = nullptr;
+  if (dm_out.has_value()) {           // + the dropout backward of dx and ITS column sums (not dx's)
+    TORCH_CHECK(!dx_sum, "norm_bwd_fused: dm_out and dx_sum are exclusive");
+    check_contig_bf16(*dm_out, "dm_out");
+    TORCH_CHECK(dm_out->sizes() == dy.sizes(), "norm_bwd_fused: dm_out shape");
+    dm = dm_out->data_ptr();
+  }
+  const int64_t K = (rms ? 1 : 2) + ((dx_sum || dm) ? 1 : 0);
   auto part = at::empty({K, (int64_t)dltb_norm_bwd_fused_blocks((int)N), d}, dy.options().dtype(at::kFloat));
   dltb_norm_bwd_fused(dy.data_ptr(), s.data_ptr(), w.data_ptr(), rms ? nullptr : mean->data_ptr<float>(),
                       rstd.data_ptr<float>(), dres.has_value() ? dres->data_ptr() : nullptr, dx.data_ptr(),
-                      part.data_ptr<float>(), (int)N, (int)d, rms, dx_sum, cur_stream());
+                      part.data_ptr<float>(), (int)N, (int)d, rms, dx_sum, cur_stream(), dm,
+                      dm ? thr_of(drop_p) : 0u, scale_of(drop_p), dm ? seed_ptr(seed, drop_p) : nullptr, site);
   return {dx, part};
 }
 
@@ -768,7 +777,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_bwd_dx", &norm_bwd_dx);
   m.def("norm_bwd_dgamma", &norm_bwd_dgamma);
   m.def("norm_bwd_fused", &norm_bwd_fused, py::arg("dy"), py::arg("s"), py::arg("w"), py::arg("mean"),
-        py::arg("rstd"), py::arg("dres"), py::arg("rms"), py::arg("dx_sum"), py::arg("dx_out") = py::none());
+        py::arg("rstd"), py::arg("dres"), py::arg("rms"), py::arg("dx_sum"), py::arg("dx_out") = py::none(),
+        py::arg("dm_out") = py::none(), py::arg("drop_p") = 0.0, py::arg("seed") = py::none(),
+        py::arg("site") = 0);
   m.def("norm_bwd_fused_supported", [](int64_t d) { return dltb_norm_bwd_fused_supported((int)d); });
   m.def("colpart", &colpart);
   m.def("gemm", &gemm, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("bias"), py::arg("tn"),

@@ -22,9 +22,11 @@ void dltb_norm_bwd(const void* dy, const void* s, const void* w, const float* me
 // fused dx + column partials; part: [(rms ? 1 : 2) + dxsum][blocks(N)][d] fp32
 bool dltb_norm_bwd_fused_supported(int d);
 int dltb_norm_bwd_fused_blocks(int N);
+// dm != nullptr: also dm = dropout_bwd(dx) (site / thr16 / drop_scale / seed) and its column sums
 bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
                          const float* rstd, const void* dres, void* dx, float* part, int N, int d,
-                         bool rms, bool dxsum, hipStream_t st);
+                         bool rms, bool dxsum, hipStream_t st, void* dm = nullptr, uint32_t thr16 = 0,
+                         float drop_scale = 1.f, const int64_t* seed = nullptr, int64_t site = 0);
 
 // elementwise.hip
 void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st);

@@ -169,14 +169,21 @@ __global__ __launch_bounds__(256) void norm_bwd_dx_kernel(
 // norm_bwd_dx + a colpart launch.
 constexpr int kFusedWaves = 8;     // 512-thread blocks: two waves per SIMD at one block per CU
 
-template <int NV, bool RMS, bool HAS_RES_GRAD, bool DXSUM>
+// XS (extra column sum): 0 none; 1 the stored dx; 2 the dropout backward of dx, dm = keep * dx / (1-p)
+// with the keep bits of dropout site `site` (bitwise the colpart DROP kernel's dm), stored to `dm`,
+// and its column sums -- the gradient of the previous block's MLP dropout and fc2 bias, produced
+// here while dx is in registers (one colpart launch less per layer).
+template <int NV, bool RMS, bool HAS_RES_GRAD, int XS>
 __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N, int d,
-    int rpw) {
+    int rpw, bf16_t* __restrict__ dm, uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr,
+    int64_t site) {
   extern __shared__ __attribute__((aligned(16))) float fold[];   // [kFusedWaves][d]
+  constexpr bool DXSUM = XS != 0;
   constexpr int K = (RMS ? 1 : 2) + (DXSUM ? 1 : 0);
+  const uint64_t dseed = (XS == 2 && thr16) ? site_seed(seed_ptr, site) : 0ull;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nvec = d >> 3;
   float wv[NV][8], acc[K][NV][8];
@@ -234,6 +241,20 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
         *reinterpret_cast<uint4*>(dx + base + idx * 8) = ov;
         if (DXSUM) {
           unpack8(ov, o);                                // sum the rounded dx the next GEMM reads
+          if (XS == 2) {
+            if (thr16) {
+              const uint32_t rk = rng_row_key(dseed, (uint32_t)row);
+#pragma unroll
+              for (int e = 0; e < 8; e += 2) {
+                const uint32_t hh = rng_pair(rk, rng_col_key(dseed, (uint32_t)(idx * 8 + e)));
+                o[e] = keep_lo(hh, thr16) ? o[e] * drop_scale : 0.f;
+                o[e + 1] = keep_hi(hh, thr16) ? o[e + 1] * drop_scale : 0.f;
+              }
+            }
+            const uint4 mv = pack8(o);
+            *reinterpret_cast<uint4*>(dm + base + idx * 8) = mv;
+            unpack8(mv, o);                              // sum the rounded dm the fc2 GEMMs read
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[K - 1][j][e] += o[e];
         }
@@ -458,31 +479,43 @@ int dltb_norm_bwd_fused_blocks(int N) { return cdiv(N, kFusedWaves * dltb_norm_b
 bool dltb_norm_bwd_fused_supported(int d) { return d % 8 == 0 && nv_for(d) <= 4; }
 
 namespace {
-template <int NV, bool RMS, bool RES, bool DXSUM>
+struct FusedDrop {
+  bf16_t* dm;
+  uint32_t thr16;
+  float scale;
+  const int64_t* seed;
+  int64_t site;
+};
+template <int NV, bool RMS, bool RES, int XS>
 void launch_bwd_fused(int N, int d, hipStream_t st, const bf16_t* dy, const bf16_t* s, const bf16_t* w,
-                      const float* mean, const float* rstd, const bf16_t* dres, bf16_t* dx, float* part) {
+                      const float* mean, const float* rstd, const bf16_t* dres, bf16_t* dx, float* part,
+                      const FusedDrop& fd) {
   const int rpw = dltb_norm_bwd_fused_rpw(N);
-  hipLaunchKernelGGL((norm_bwd_fused_kernel<NV, RMS, RES, DXSUM>), dim3(dltb_norm_bwd_fused_blocks(N)),
+  hipLaunchKernelGGL((norm_bwd_fused_kernel<NV, RMS, RES, XS>), dim3(dltb_norm_bwd_fused_blocks(N)),
                      dim3(kFusedWaves * 64), (size_t)kFusedWaves * d * sizeof(float), st, dy, s, w, mean, rstd, dres, dx,
-                     part, N, d, rpw);
+                     part, N, d, rpw, fd.dm, fd.thr16, fd.scale, fd.seed, fd.site);
+}
+template <int NV, bool RMS, bool RES>
+void launch_bwd_fused_xs(int xs, int N, int d, hipStream_t st, const bf16_t* dy, const bf16_t* s,
+                         const bf16_t* w, const float* mean, const float* rstd, const bf16_t* dres,
+                         bf16_t* dx, float* part, const FusedDrop& fd) {
+  if (xs == 2) launch_bwd_fused<NV, RMS, RES, 2>(N, d, st, dy, s, w, mean, rstd, dres, dx, part, fd);
+  else if (xs == 1) launch_bwd_fused<NV, RMS, RES, 1>(N, d, st, dy, s, w, mean, rstd, dres, dx, part, fd);
+  else launch_bwd_fused<NV, RMS, RES, 0>(N, d, st, dy, s, w, mean, rstd, dres, dx, part, fd);
 }
 template <int NV, bool RMS>
-void launch_bwd_fused_nv(bool res, bool dxsum, int N, int d, hipStream_t st, const bf16_t* dy,
+void launch_bwd_fused_nv(bool res, int xs, int N, int d, hipStream_t st, const bf16_t* dy,
                          const bf16_t* s, const bf16_t* w, const float* mean, const float* rstd,
-                         const bf16_t* dres, bf16_t* dx, float* part) {
-  if (res) {
-    if (dxsum) launch_bwd_fused<NV, RMS, true, true>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
-    else launch_bwd_fused<NV, RMS, true, false>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
-  } else {
-    if (dxsum) launch_bwd_fused<NV, RMS, false, true>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
-    else launch_bwd_fused<NV, RMS, false, false>(N, d, st, dy, s, w, mean, rstd, dres, dx, part);
-  }
+                         const bf16_t* dres, bf16_t* dx, float* part, const FusedDrop& fd) {
+  if (res) launch_bwd_fused_xs<NV, RMS, true>(xs, N, d, st, dy, s, w, mean, rstd, dres, dx, part, fd);
+  else launch_bwd_fused_xs<NV, RMS, false>(xs, N, d, st, dy, s, w, mean, rstd, dres, dx, part, fd);
 }
 }  // namespace
 
 bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
                          const float* rstd, const void* dres, void* dx, float* part, int N, int d,
-                         bool rms, bool dxsum, hipStream_t st) {
+                         bool rms, bool dxsum, hipStream_t st, void* dm, uint32_t thr16, float drop_scale,
+                         const int64_t* seed, int64_t site) {
   if (!dltb_norm_bwd_fused_supported(d)) return false;
   auto DY = (const bf16_t*)dy;
   auto S = (const bf16_t*)s;
@@ -490,10 +523,12 @@ bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const flo
   auto DR = (const bf16_t*)dres;
   auto DX = (bf16_t*)dx;
   const bool res = dres != nullptr;
-#define DLTB_NBF(NVV)                                                                                 \
-  do {                                                                                                \
-    if (rms) launch_bwd_fused_nv<NVV, true>(res, dxsum, N, d, st, DY, S, W, mean, rstd, DR, DX, part);  \
-    else launch_bwd_fused_nv<NVV, false>(res, dxsum, N, d, st, DY, S, W, mean, rstd, DR, DX, part);     \
+  const int xs = dm != nullptr ? 2 : (dxsum ? 1 : 0);
+  const FusedDrop fd{(bf16_t*)dm, thr16, drop_scale, seed, site};
+#define DLTB_NBF(NVV)                                                                                    \
+  do {                                                                                                   \
+    if (rms) launch_bwd_fused_nv<NVV, true>(res, xs, N, d, st, DY, S, W, mean, rstd, DR, DX, part, fd);  \
+    else launch_bwd_fused_nv<NVV, false>(res, xs, N, d, st, DY, S, W, mean, rstd, DR, DX, part, fd);     \
   } while (0)
   switch (nv_for(d)) {
     case 1: DLTB_NBF(1); break;

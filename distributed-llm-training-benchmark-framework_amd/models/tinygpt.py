@@ -22,6 +22,7 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
+import os
 from types import SimpleNamespace
 
 import torch
@@ -68,7 +69,12 @@ class TinyGPTBlock(nn.Module):
 # DLTB_MASK_STREAM=1: generate the attention dropout mask on a side stream, concurrent with LN1 + QKV
 _MASK_STREAM = __import__("os").environ.get("DLTB_MASK_STREAM", "0") == "1"
 # DLTB_FUSE_MLP_DROPOUT=0: x2 = x1 + Dropout(m) as its own kernel instead of inside the next LayerNorm
-_FUSE_MLP_DROPOUT = __import__("os").environ.get("DLTB_FUSE_MLP_DROPOUT", "1") == "1"
+_FUSE_MLP_DROPOUT = os.environ.get("DLTB_FUSE_MLP_DROPOUT", "1") == "1"
+# DLTB_FUSE_DROPOUT_BWD=1: the consumer's LayerNorm backward kernel forms the producing block's MLP
+# Dropout backward + fc2 bias partials (one colpart launch less per layer).  Measured neutral on
+# MI355X (7.63 vs 7.62 ms, profiles/ab_fused_dropout_bwd_1gpu.jsonl: the hash work the 8-wave norm
+# kernel takes on costs what the launch saved), so the producing block's colpart stays the default.
+_FUSE_DROPOUT_BWD = os.environ.get("DLTB_FUSE_DROPOUT_BWD", "0") == "1"
 
 
 class _EmbedFn(torch.autograd.Function):
@@ -134,14 +140,17 @@ class _BlockFn(torch.autograd.Function):
         m = F_.linear_fwd(g, w2, b2)        # Dropout(m) + x1 happens in the consumer's LayerNorm
         rt.release_forward(unit)
         ctx.model, ctx.i, ctx.lb = model, i, lb
+        ctx.fused_prev = m_in is not None   # LN1 applied the previous block's MLP dropout
         ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g)
         if not _FUSE_MLP_DROPOUT:           # standalone residual + dropout kernel
             return F_.dropout(x1, m, p, rt.seed, model.site_mlp(i)), None
         return x1, m
 
     @staticmethod
-    def backward(ctx, dx2, dm_unused):
-        # dx2 = d(x1 + Dropout(m)) from the consumer; m's gradient (Dropout backward) is formed here
+    def backward(ctx, dx2, dm_in):
+        # dx2 = d(x1 + Dropout(m)) from the consumer.  m's gradient (Dropout backward, with the fc2
+        # bias column sum) either comes from the consumer's LayerNorm backward (dm_in, engines with
+        # grad_write_ahead) or is formed here
         model, i = ctx.model, ctx.i
         rt, unit = model.rt, model.unit_blocks[i]
         (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g) = ctx.saved
@@ -167,8 +176,11 @@ class _BlockFn(torch.autograd.Function):
         shared = rt.grad_reducer()
         red = shared if shared is not None else F_.GradReducer()
         # MLP
-        dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
-                                 out=lb and lb.dm)
+        if dm_in is not None:
+            dm = dm_in
+        else:
+            dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
+                                     out=lb and lb.dm)
         wgrad(10, dm, g)
         dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
         df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
@@ -186,14 +198,23 @@ class _BlockFn(torch.autograd.Function):
         par.join()                                            # dQ (side) completes dqkv
         wgrad(2, dqkv, h1)
         dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
+        drop_prev = None
+        if ctx.fused_prev and rt.grad_write_ahead and _FUSE_DROPOUT_BWD:
+            # the previous block's Dropout(m') backward + fc2 bias sum, produced with dx in one kernel
+            ps = rt.grad_slot(model.unit_blocks[i - 1], 11)
+            plb = model.layer_buffer(i - 1) if lb is not None else None
+            drop_prev = (p, rt.seed, model.site_mlp(i - 1), plb and plb.dm, ps[0], ps[1])
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False, par,
-                         red, bias=(dqkv, s[3][0], s[3][1]))
+                         red, bias=(dqkv, s[3][0], s[3][1]), drop=drop_prev)
+        dm_prev = None
+        if drop_prev is not None:
+            dx, dm_prev = dx
         if shared is None:
             red.flush()
         par.join()                                            # all of this unit's gradients written
         rt.grads_ready(unit)
         rt.release_backward(unit)
-        return dx, None, None, None
+        return dx, dm_prev, None, None
 
 
 class _HeadFn(torch.autograd.Function):

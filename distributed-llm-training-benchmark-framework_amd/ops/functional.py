@@ -89,12 +89,41 @@ class GradReducer:
 
 
 def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=None, bias=None,
-             dx_out=None):
+             dx_out=None, drop=None):
     """dx on the current stream; dgamma/dbeta (parameter gradients) on ``par``'s side stream.
 
     With a :class:`GradReducer` the dgamma/dbeta partials (and, with ``bias=(src, slot, acc)``, the
     column sum of ``src`` -- ``src="dx"`` meaning this call's output) come from ONE colpart launch
-    and are reduced at ``red.flush()``."""
+    and are reduced at ``red.flush()``.
+
+    ``drop=(p, seed, site, dm_out, db, db_acc)``: also return dm = Dropout_backward(dx) of dropout
+    site ``site`` with its column sum into ``db`` -- ``(dx, dm)`` -- fused into the same kernel on
+    the GPU (the previous block's MLP dropout and fc2 bias gradient)."""
+    if drop is not None:
+        dp, dseed, dsite, dm_out, db, db_acc = drop
+        if red is not None and _gpu(dy) and _FUSED_NORM_BWD and ext().norm_bwd_fused_supported(dy.shape[-1]):
+            C = ext()
+            dm = torch.empty_like(dy) if dm_out is None else dm_out
+            dx, part = C.norm_bwd_fused(dy, s, w, mean, rstd, dres, rms, False, dx_out, dm, dp,
+                                        _sd(dseed) if dp > 0 else None, dsite)
+            red.add(part[0], gw, accumulate)
+            if not rms:
+                red.add(part[1], gb, accumulate)
+            red.add(part[-1], db, db_acc)
+            if bias is not None and bias[1] is not None:
+                assert not isinstance(bias[0], str), "drop and a dx bias sum are exclusive"
+                if red.defer_plain:
+                    red.pending.append((bias[0], bias[1], bias[2]))
+                else:
+                    parts = C.colpart([_PLAIN], [bias[0]], [None], [None], [None], [None], 0.0, None, [0])
+                    red.add(parts[0][0], bias[1], bias[2])
+            return dx, dm
+        dx = norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par, red, bias, dx_out)
+        red_local = red if red is not None else GradReducer()
+        dm = dropout_bwd_bias(dx, dp, dseed, dsite, db, db_acc, red_local, out=dm_out)
+        if red is None:
+            red_local.flush()
+        return dx, dm
     if red is not None:
         if _gpu(dy) and _FUSED_NORM_BWD and ext().norm_bwd_fused_supported(dy.shape[-1]):
             # one kernel: dx + gamma / beta partials (+ the column partials of dx itself)

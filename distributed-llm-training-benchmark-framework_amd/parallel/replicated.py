@@ -33,6 +33,7 @@ from .wgrad import WgradQueue
 
 class ReplicatedEngine(Engine):
     name = "ddp"
+    grad_write_ahead = True      # every gradient slot is a view of the flat buffer from the start
 
     def _setup(self):
         cfg, model = self.cfg, self.model

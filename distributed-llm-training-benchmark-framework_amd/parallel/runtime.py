@@ -83,6 +83,9 @@ class ParamRuntime:
         return p.grad, True
 
     # weight gradients (dW (+)= dY^T X of a linear layer)
+    # True: a gradient slot of a unit may be written before that unit's own backward runs (the
+    # consumer block forms the previous block's fc2 bias gradient, models/tinygpt.py)
+    grad_write_ahead = False
     defer_wgrad = False     # True: the engine queues them (parallel/wgrad.py) and issues batches
     # order of the blocks' gradient slots in the engine's flat buffer: True = last block first
     # (backward-ordered replicated layouts); the model's layer-strided buffers follow it

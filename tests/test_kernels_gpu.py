@@ -187,6 +187,33 @@ def test_norm_bwd_fused(N, d, rms, bias_src):
         close(bslot, ext_src.float().sum(0), 0.5, 2e-2, "external column sum")
 
 
+@pytest.mark.parametrize("N,d", [(2048, 1024), (300, 768)])
+@pytest.mark.parametrize("p", [0.1, 0.0])
+def test_norm_bwd_fused_dropout(N, d, p):
+    """LayerNorm backward that also forms the previous layer's Dropout backward dm of its dx (and
+    dm's column sum): dm bitwise the standalone dropout kernel's, dx as without it."""
+    from dltb.ops import functional as F_
+    dy, s_, dres = rnd(N, d), rnd(N, d), rnd(N, d)
+    w = rnd(d, scale=0.5) + 1
+    mean = torch.randn(N, device=DEV) * 0.1
+    rstd = torch.rand(N, device=DEV) + 0.5
+    sd = seed_obj(9)
+    outs = [torch.zeros(d, device=DEV, dtype=torch.bfloat16) for _ in range(3)]
+    red = F_.GradReducer()
+    dx, dm = F_.norm_bwd(dy, s_, w, mean, rstd, dres, outs[0], outs[1], False, False, red=red,
+                         drop=(p, sd, 7, None, outs[2], False))
+    red.flush()
+    ref_outs = [torch.zeros(d, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+    red2 = F_.GradReducer()
+    dx2 = F_.norm_bwd(dy, s_, w, mean, rstd, dres, ref_outs[0], ref_outs[1], False, False, red=red2)
+    red2.flush()
+    assert torch.equal(dx, dx2), "dx"
+    assert torch.equal(outs[0], ref_outs[0]) and torch.equal(outs[1], ref_outs[1]), "dgamma / dbeta"
+    rdm = ref.dropout(None, dx, p, sd, 7) if p > 0 else dx
+    assert torch.equal(dm, rdm), "dropout backward"
+    close(outs[2], dm.float().sum(0), 0.5, 2e-2, "dm column sum")
+
+
 @pytest.mark.parametrize("R,C", [(1024, 3072), (4096, 1024), (100, 36)])
 def test_transpose_into(R, C):
     C_ = ext()
