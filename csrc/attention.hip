@@ -28,6 +28,8 @@
 // 8(i>>2) + 4h of query q — so forward and dQ lanes read one coalesced word per 64-key tile and the
 // dK/dV kernel stages 4 words per query row in LDS.  The hash runs 1x instead of 3x, and the
 // softmax kernels pay 2 VALU ops per probability for dropout.
+#include <cstdlib>
+
 #include "common.h"
 #include "mfma_tiles.h"
 
@@ -56,6 +58,8 @@ struct AttnArgs {
   float drop_scale;
   const int64_t* seed_ptr;
   int64_t site;
+  int gsplit;       // bwd_dkdv: workgroups per KV head, each summing G / gsplit query heads
+  float* part;      // bwd_dkdv with gsplit > 1: fp32 partials [gsplit][2][B*T][Hkv*D] (scaled)
 };
 
 // accumulator registers 8s .. 8s+7 -> bf16 B operand of k-step s
@@ -102,6 +106,19 @@ DLTB_DEV void store_acc_rows(bf16_t* dst_row, const f32x16* acc, float scale, in
       o.x = pack_bf2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
       o.y = pack_bf2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
       *reinterpret_cast<uint2*>(dst_row + dt * 32 + 8 * g + 4 * h) = o;
+    }
+  }
+}
+
+template <int D>
+DLTB_DEV void store_acc_rows_f32(float* dst_row, const f32x16* acc, float scale, int h) {
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 o = {acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale,
+                        acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale};
+      *reinterpret_cast<float4*>(dst_row + dt * 32 + 8 * g + 4 * h) = o;
     }
   }
 }
@@ -430,10 +447,15 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const int kw = w & 3, sp = w >> 2, stid = tid & 255;
   const int T = P.T, nT = T / kTile;
   int kb, bk;
-  block_coords(T / kBlockRows, P.B * P.Hkv, false, kb, bk);
-  if (CAUSAL) kb = T / kBlockRows - 1 - kb;      // heaviest key blocks (first keys) ... last
+  const int gsplit = P.gsplit;
+  block_coords(T / kBlockRows, P.B * P.Hkv * gsplit, false, kb, bk);
+  const int gs = bk % gsplit;
+  bk /= gsplit;
+  // one workgroup per key block: all resident at once, heaviest (first keys) last.  Head-split
+  // grids (causal GQA) are several waves deep, so they go heaviest first (greedy balance)
+  if (CAUSAL && gsplit == 1) kb = T / kBlockRows - 1 - kb;
   const int b = bk / P.Hkv, hk = bk % P.Hkv;
-  const int G = P.Hq / P.Hkv;
+  const int G = P.Hq / P.Hkv / gsplit, g0 = gs * G;   // this workgroup's query heads of the group
   const int kblk0 = kb * kBlockRows;
   const int k0 = kblk0 + kw * 32;
   const int key = k0 + r;
@@ -466,12 +488,12 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const int wv = __builtin_amdgcn_readfirstlane(kw);
   float vl = 0.f, vd = 0.f;
   uint32_t mword = 0;
-  auto tile_of = [&](int j, int& g, int& t) { g = j / nit; t = t_begin + (j % nit) * KS + sp; };
+  auto tile_of = [&](int j, int& g, int& t) { g = g0 + j / nit; t = t_begin + (j % nit) * KS + sp; };
   auto load = [&](int j) {
     int g, t;
     tile_of(j, g, t);
     if (t >= nT) return;
-    const int hq = hk * G + g;
+    const int hq = hk * G * gsplit + g;
     const long bq = (long)b * P.Hq + hq;
     // Q / dO tiles straight into the stage buffer by LDS-DMA (it is not being read: the previous
     // reader of this buffer finished before the last barrier)
@@ -656,10 +678,49 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
         }
   }
   const float s_drop = DROP ? P.drop_scale : 1.f;
+  if (gsplit > 1) {      // partial over this workgroup's heads -> fp32, summed by dkdv_reduce_kernel
+    const long plane = (long)P.B * T * P.Hkv * D;
+    float* pk = P.part + 2 * gs * plane + ((long)b * T + key) * P.Hkv * D + hk * D;
+    store_acc_rows_f32<D>(pk, dk, P.scale * s_drop, h);
+    store_acc_rows_f32<D>(pk + plane, dv, s_drop, h);
+    return;
+  }
   bf16_t* dkrow = P.out + ((long)b * T + key) * P.out_stride + hk * D;
   bf16_t* dvrow = P.out2 + ((long)b * T + key) * P.out2_stride + hk * D;
   store_acc_rows<D>(dkrow, dk, P.scale * s_drop, h);
   store_acc_rows<D>(dvrow, dv, s_drop, h);
+}
+
+// dK / dV = sum of the head-split partials (8 columns per thread), bf16 into the strided outputs
+__global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restrict__ part, int gsplit,
+                                                          long rows, int cols, bf16_t* __restrict__ dk,
+                                                          long dks, bf16_t* __restrict__ dv, long dvs) {
+  const long plane = rows * cols;
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= 2 * plane) return;
+  const int which = i >= plane;
+  const long e = i - which * plane;
+  float a[8];
+  {
+    const float4 x0 = *reinterpret_cast<const float4*>(part + i);
+    const float4 x1 = *reinterpret_cast<const float4*>(part + i + 4);
+    a[0] = x0.x; a[1] = x0.y; a[2] = x0.z; a[3] = x0.w; a[4] = x1.x; a[5] = x1.y; a[6] = x1.z; a[7] = x1.w;
+  }
+  for (int s = 1; s < gsplit; ++s) {
+    const float* src = part + 2 * s * plane + i;
+    const float4 x0 = *reinterpret_cast<const float4*>(src);
+    const float4 x1 = *reinterpret_cast<const float4*>(src + 4);
+    a[0] += x0.x; a[1] += x0.y; a[2] += x0.z; a[3] += x0.w;
+    a[4] += x1.x; a[5] += x1.y; a[6] += x1.z; a[7] += x1.w;
+  }
+  const long r = e / cols, c = e % cols;
+  bf16_t* dst = which ? dv + r * dvs + c : dk + r * dks + c;
+  uint4 o;
+  o.x = pack_bf2(a[0], a[1]);
+  o.y = pack_bf2(a[2], a[3]);
+  o.z = pack_bf2(a[4], a[5]);
+  o.w = pack_bf2(a[6], a[7]);
+  *reinterpret_cast<uint4*>(dst) = o;
 }
 
 // =============================================================================== dQ
@@ -863,6 +924,7 @@ AttnArgs make_args(const void* q, const void* k, const void* v, long qs, long ks
   a.drop_scale = drop_scale;
   a.seed_ptr = seed;
   a.site = site;
+  a.gsplit = 1;
   return a;
 }
 
@@ -959,8 +1021,14 @@ namespace {
 template <int D, bool C, bool DR>
 void launch_dkdv(const AttnArgs& a, hipStream_t st) {
   constexpr int KS = dkdv_ks<D>();
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hkv), dim3(256 * KS),
-                     dkdv_smem_bytes<D>(), st, a);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hkv * a.gsplit),
+                     dim3(256 * KS), dkdv_smem_bytes<D>(), st, a);
+  if (a.gsplit > 1) {
+    const long rows = (long)a.B * a.T;
+    const int cols = a.Hkv * D;
+    hipLaunchKernelGGL(dkdv_reduce_kernel, dim3(cdiv(2 * rows * cols / 8, 256)), dim3(256), 0, st,
+                       a.part, a.gsplit, rows, cols, a.out, a.out_stride, a.out2, a.out2_stride);
+  }
 }
 template <int D, bool C, bool DR>
 void launch_dq(const AttnArgs& a, hipStream_t st) {
@@ -970,14 +1038,39 @@ void launch_dq(const AttnArgs& a, hipStream_t st) {
 }
 }  // namespace
 
+// The dK/dV grid has one workgroup (4 waves, 1 wave / SIMD at D = 128) per key block and KV head.
+// A causal grid is unbalanced (key block 0 sees every query tile, the last one a single tile) and
+// when it is no deeper than the chip (Mistral-7B shape: 32 key blocks x 8 KV heads = 256) the
+// step waits for the heaviest workgroup.  Splitting the G query heads of each KV group over
+// several workgroups (fp32 partials + one reduce) makes the grid several waves deep, dispatched
+// heaviest first.  DLTB_DKDV_GSPLIT = n forces n (1 = off).
+int dltb_attn_dkdv_gsplit(int B, int T, int Hq, int Hkv, int causal) {
+  const int G = Hq / Hkv;
+  if (!causal || G < 2) return 1;
+  static const int forced = [] {
+    const char* e = getenv("DLTB_DKDV_GSPLIT");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced > 0) return G % forced == 0 ? forced : 1;
+  const long wgs = (long)(T / kBlockRows) * B * Hkv;
+  int s = 1;
+  while (s < G && wgs * s < 2L * 256 && G % (2 * s) == 0) s *= 2;
+  return s;
+}
+
 // part: 0 = dK/dV (key-major kernel), 1 = dQ (query-major kernel); both need delta
 void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, const void* dout,
                         const float* lse, const float* delta, const uint32_t* mask, void* out,
                         void* out2, long qs, long ks, long vs, long dos, long outs, long out2s,
                         int B, int T, int Hq, int Hkv, int D, float scale, int causal,
-                        uint32_t thr16, float drop_scale, hipStream_t st, const void* o, long os) {
+                        uint32_t thr16, float drop_scale, hipStream_t st, const void* o, long os,
+                        int gsplit, float* part_buf) {
   AttnArgs a = make_args(q, k, v, qs, ks, vs, B, T, Hq, Hkv, scale, causal, thr16, drop_scale,
                          nullptr, 0);
+  if (part == 0 && gsplit > 1 && part_buf && (Hq / Hkv) % gsplit == 0) {
+    a.gsplit = gsplit;
+    a.part = part_buf;
+  }
   a.dout = (const bf16_t*)dout;
   a.do_stride = dos;
   a.lse = const_cast<float*>(lse);

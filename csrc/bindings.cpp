@@ -483,12 +483,24 @@ void attn_bwd_part(int64_t part, const Tensor& q, const Tensor& k, const Tensor&
   const uint32_t thr = thr_of(p);
   const uint32_t* mp = mask_ptr(mask, thr, B, T, Hq);
   dltb_attn_init_attributes();
+  int gsplit = 1;
+  Tensor pbuf;
+  if (part == 0) {
+    gsplit = dltb_attn_dkdv_gsplit((int)B, (int)T, (int)Hq, (int)Hkv, causal ? 1 : 0);
+    const bool vec_ok = reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 &&
+                        reinterpret_cast<uintptr_t>(out2->data_ptr()) % 16 == 0 &&
+                        out.stride(0) % 8 == 0 && out2->stride(0) % 8 == 0;
+    if (!vec_ok) gsplit = 1;
+    if (gsplit > 1)
+      pbuf = at::empty({gsplit * 2 * B * T * Hkv * D}, q.options().dtype(at::kFloat));
+  }
   dltb_attn_bwd_part((int)part, q.data_ptr(), k.data_ptr(), v.data_ptr(), dout.data_ptr(),
                      lse.data_ptr<float>(), delta.data_ptr<float>(), mp, out.data_ptr(),
                      part == 0 ? out2->data_ptr() : nullptr, q.stride(0), k.stride(0), v.stride(0),
                      dout.stride(0), out.stride(0), part == 0 ? out2->stride(0) : 0, (int)B, (int)T,
                      (int)Hq, (int)Hkv, (int)D, (float)scale, causal ? 1 : 0, thr, scale_of(p),
-                     cur_stream(), o.has_value() ? o->data_ptr() : nullptr, o.has_value() ? o->stride(0) : 0);
+                     cur_stream(), o.has_value() ? o->data_ptr() : nullptr, o.has_value() ? o->stride(0) : 0,
+                     gsplit, gsplit > 1 ? pbuf.data_ptr<float>() : nullptr);
 }
 
 void attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,

@@ -94,7 +94,9 @@ void dltb_attn_bwd_part(int part, const void* q, const void* k, const void* v, c
                         void* out2, long qs, long ks, long vs, long dos, long outs, long out2s,
                         int B, int T, int Hq, int Hkv, int D, float scale, int causal,
                         uint32_t thr16, float drop_scale, hipStream_t st, const void* o = nullptr,
-                        long os = 0);
+                        long os = 0, int gsplit = 1, float* part_buf = nullptr);
+// dK/dV workgroups per KV head for a causal GQA backward (1 = one workgroup sums the whole group)
+int dltb_attn_dkdv_gsplit(int B, int T, int Hq, int Hkv, int causal);
 void dltb_attn_init_attributes();
 
 // ---- batched column reductions (colreduce.hip)

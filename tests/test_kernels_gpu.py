@@ -365,6 +365,9 @@ ATTN_CASES = [
     (1, 512, 2, 2, 64, True, 0.0),
     (1, 256, 8, 2, 128, True, 0.0),
     (1, 256, 4, 4, 128, False, 0.1),
+    # causal GQA: the dK/dV pass splits each KV group's query heads over workgroups (fp32 partials)
+    (1, 512, 8, 2, 128, True, 0.1),
+    (2, 256, 4, 2, 64, True, 0.1),
 ]
 
 
