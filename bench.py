@@ -51,6 +51,10 @@ def main():
     ap.add_argument("--grad-accum", type=int, default=4)
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--accum-semantics", default="reference", choices=["reference", "uniform"])
+    ap.add_argument("--grad-reduce", default="auto", choices=["auto", "micro", "window"],
+                    help="ZeRO-2 gradient reduce-scatter: every micro-step (DeepSpeed) or once per "
+                         "accumulation window; auto = window on N > 1 (xGMI is point-to-point: 1/4 "
+                         "of the traffic), no collective at all on N = 1")
     ap.add_argument("--no-align", action="store_true", help="do not align warmup to accumulation windows")
     ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
                     help="replay each micro-step as a captured HIP graph (DLTB_GRAPHS overrides)")
@@ -79,9 +83,12 @@ def main():
     mcfg = get_model_config(args.tier, args.seq_len)
     with torch.device(device):          # random init straight into HBM (7B-class models never touch host RAM)
         model = build_model(mcfg)
+    grad_reduce = args.grad_reduce
+    if grad_reduce == "auto":
+        grad_reduce = "window" if (world > 1 and args.strategy == "zero2") else "micro"
     h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None,
                            grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype="bf16",
-                           bucket_mb=args.bucket_mb, seed=42)
+                           bucket_mb=args.bucket_mb, seed=42, grad_reduce=grad_reduce)
     engine, ecfg = _engine_for(h, model, device)
     ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
     batches = make_batcher("device", ds, args.per_device_batch, world, rank, args.strategy, device)
@@ -142,7 +149,8 @@ def main():
                        "micro_batch_per_gpu": args.per_device_batch,
                        "grad_accum": accum,
                        "seq_len": args.seq_len,
-                       "parallelism": f"{args.strategy}-dp{world}"},
+                       "parallelism": f"{args.strategy}-dp{world}",
+                       "grad_reduce": grad_reduce if args.strategy == "zero2" else None},
             "strategy": args.strategy,
             "optimizer_steps_timed": opt_steps,
             "peak_hbm_gb": peak_gb,

@@ -12,7 +12,7 @@ Differences that make the numbers honest (recorded in the extended sidecar):
 * the timed region is bracketed by a barrier and a device synchronisation; mean step time is the
   synchronised wall time of the post-warmup steps divided by their count, max over ranks;
 * per-step losses stay on the device and are read once at the end (the reference syncs every step).
-Extra flags (all optional): --accum-semantics, --dtype, --device, --bucket-mb, --dropout, --seed,
+Extra flags (all optional): --accum-semantics, --grad-reduce, --dtype, --device, --bucket-mb, --dropout, --seed,
 --profile, --debug-collectives, --fail-at-step, --timeout-min, --data-loader, --model-tier.
 """
 import argparse
@@ -66,6 +66,9 @@ def build_parser():
     p.add_argument("--results-dir", type=str, required=True)
     # MI355X extras
     p.add_argument("--accum-semantics", choices=["reference", "uniform"], default="reference")
+    p.add_argument("--grad-reduce", choices=["micro", "window"], default="micro",
+                   help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed) or once per "
+                        "accumulation window")
     p.add_argument("--dtype", choices=list(DTYPES), default="bf16")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda" if torch.cuda.is_available() else "cpu")
     p.add_argument("--bucket-mb", type=float, default=64.0, help="gradient bucket cap (MiB)")
@@ -105,7 +108,8 @@ def _engine_for(args, model, device):
         if path and os.path.exists(path):
             fc = load_fsdp_config(path)
     cfg = engine_config(args.strategy, args.grad_accum, args.accum_semantics, ds, fc,
-                        compute_dtype=DTYPES[args.dtype], bucket_mb=args.bucket_mb, seed=args.seed)
+                        compute_dtype=DTYPES[args.dtype], bucket_mb=args.bucket_mb, seed=args.seed,
+                        grad_reduce=getattr(args, "grad_reduce", "micro"))
     return make_engine(model, cfg, device), cfg
 
 
@@ -261,7 +265,7 @@ def train(args):
             "comm_topology": comm_describe(world) if (is_main and device.type == "cuda") else None,
             "memory": engine.memory_report(),
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
-            "accum_semantics": args.accum_semantics, "dtype": args.dtype, "data_loader": args.data_loader,
+            "accum_semantics": args.accum_semantics, "grad_reduce": args.grad_reduce, "dtype": args.dtype, "data_loader": args.data_loader,
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
             "phase_times_ms": timers.summary() if timers is not None else None,
         }

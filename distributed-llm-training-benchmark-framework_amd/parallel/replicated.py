@@ -18,6 +18,11 @@ DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
   (one float all-reduce), clipping coefficient on device, fused AdamW on the owner shard writing
   the bf16 chunk in place, then an in-place all-gather per bucket re-replicates the parameters.
 * ZeRO-1: like ZeRO-2 but gradients accumulate unsharded and are reduce-scattered at the boundary.
+  This is also ZeRO-2 with ``--grad-reduce window`` (bench.py's default on N > 1).  xGMI links are
+  point-to-point, so a ring reduce-scatter is per-link bound, and one reduce-scatter per window
+  moves 1/grad_accum of the per-micro-step traffic.  The flat gradient buffer is full-size in both
+  modes, so HBM use is the same.  Micro-steps without a collective leave every dW product queued
+  for one batched flush, as at world size 1.
 """
 import os
 
@@ -68,7 +73,7 @@ class ReplicatedEngine(Engine):
             self.rs_out = torch.zeros(L.owner_numel, dtype=dt, device=dev) if self.world > 1 else None
             # ws == 1: nothing to reduce, gradients accumulate in place in the bf16 flat buffer
             self.acc = torch.zeros(L.owner_numel, dtype=torch.float32, device=dev) \
-                if (self.accum > 1 and self.world > 1) else None
+                if (self.stage == 2 and self.accum > 1 and self.world > 1) else None
         else:
             master = master_full
             opt_segs = [(0, L.total, self.flat_param)]
@@ -198,11 +203,11 @@ class ReplicatedEngine(Engine):
         if b is None:
             return
         self._pending[b] -= 1
-        if self._pending[b] == 0:
-            if self.world > 1:
-                self._wq.flush(self.layout.buckets[b].units)    # this bucket's dW, then its collective
-            if self._reduce_now():
-                self._launch(b)
+        if self._pending[b] == 0 and self._reduce_now():
+            self._wq.flush(self.layout.buckets[b].units)        # this bucket's dW, then its collective
+            self._launch(b)
+        # (micro-steps without a collective -- inside a ZeRO-1 / window-reduced accumulation
+        # window -- leave every dW queued for the single batched flush at the end of the backward)
 
     def _launch(self, b):
         bk = self.layout.buckets[b]

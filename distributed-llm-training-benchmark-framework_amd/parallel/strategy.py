@@ -56,7 +56,15 @@ def load_fsdp_config(path: str) -> dict:
 def engine_config(strategy: str, grad_accum: int = 1, semantics: str = "reference",
                   ds_config: Optional[dict] = None, fsdp_config: Optional[dict] = None,
                   compute_dtype=torch.bfloat16, bucket_mb: float = 64.0, seed: int = 42,
-                  overrides: Optional[dict] = None) -> EngineConfig:
+                  overrides: Optional[dict] = None, grad_reduce: str = "micro") -> EngineConfig:
+    """``grad_reduce`` (ZeRO-2 only): ``micro`` reduce-scatters the gradients after every micro-step
+    (DeepSpeed stage 2, configs/deepspeed/zero2.json); ``window`` accumulates them locally over the
+    ``grad_accum`` window and reduce-scatters once, during the boundary micro-step's backward
+    (ZeRO-1 communication: 1/grad_accum of the xGMI traffic).  Optimizer state stays sharded
+    either way, and the engine's flat gradient buffer is full-size in both modes, so HBM is the
+    same."""
+    if grad_reduce not in ("micro", "window"):
+        raise ValueError(f"grad_reduce must be micro or window, not {grad_reduce}")
     if strategy not in STRATEGIES:
         raise ValueError(f"unknown strategy {strategy}")
     cfg = EngineConfig(strategy=strategy, compute_dtype=compute_dtype, bucket_mb=bucket_mb, seed=seed)
@@ -80,6 +88,9 @@ def engine_config(strategy: str, grad_accum: int = 1, semantics: str = "referenc
     z = ds.get("zero_optimization", {}) or {}
     if strategy == "zero2":
         cfg.zero_stage = int(z.get("stage", 2)) if int(z.get("stage", 2)) in (1, 2) else 2
+        if grad_reduce == "window":
+            cfg.zero_stage = 1
+        cfg.extra["grad_reduce"] = "window" if cfg.zero_stage == 1 else "micro"
         rb = _num(z.get("reduce_bucket_size"))
         if rb:
             cfg.extra["reduce_bucket_elems"] = int(rb)

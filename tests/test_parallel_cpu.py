@@ -135,6 +135,7 @@ def _worker(rank, world, port, strategy, accum, kw, out_path, global_batch=4):
     ("ddp", 1, {}),
     ("ddp", 2, {"semantics": "uniform"}),
     ("zero2", 2, {}),
+    ("zero2", 2, {"zero_stage": 1}),       # --grad-reduce window: one reduce-scatter per window
     ("zero3", 2, {}),
     ("zero3", 1, {"max_live": 0}),
     ("fsdp", 1, {}),
@@ -154,7 +155,8 @@ def test_world2_matches_single_process(strategy, accum, kw):
         assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
 
 
-@pytest.mark.parametrize("strategy,accum,kw", [("zero2", 2, {}), ("zero3", 2, {}), ("ddp", 1, {}),
+@pytest.mark.parametrize("strategy,accum,kw", [("zero2", 2, {}), ("zero2", 2, {"zero_stage": 1}),
+                                               ("zero3", 2, {}), ("ddp", 1, {}),
                                                ("fsdp", 1, {})])
 def test_world4_matches_single_process(strategy, accum, kw):
     """Four ranks (uneven bucket chunks, padding on every rank, prefetch across 4 shards) reproduce
