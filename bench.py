@@ -5,31 +5,76 @@ Metric and config are the ones BASELINE.json names: tokens/sec (+ step time + pe
 Tier A (236.4M params, d1024 / 16 heads / 16 layers, vocab 32000), seq 2048, per-device batch 1,
 grad-accum 4, default strategy ZeRO-2 (the reference's headline: 18,147 tok/s on 4x A10), bf16,
 synthetic tokens, random init.  A "step" is one micro-batch, as in the reference
-(train_harness.py:351-393); ZeRO-2 runs its optimizer step (fused AdamW + clip + WarmupLR + bf16
-all-gather) at every 4th micro-step, and the timed region is aligned to whole accumulation windows
-so it contains exactly steps/4 optimizer steps.
+(train_harness.py:351-393).  ZeRO-2 is DeepSpeed stage 2 at every world size: the gradients are
+reduce-scattered after EVERY micro-step (configs/deepspeed/zero2.json, ``reduce_scatter: true``)
+and the optimizer step (fused AdamW + clip + WarmupLR + bf16 all-gather) runs at every 4th
+micro-step; ``--grad-reduce window`` (one reduce-scatter per accumulation window) is ZeRO-1
+communication and is labelled ``zero1-dpN``.  Any K consecutive micro-steps contain K/4 optimizer
+steps, so the timed region needs no alignment: exactly W warm-up steps run, then exactly K are
+timed.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--strategy zero2|ddp|fsdp|zero3]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Launch modes (reference: scripts/launch_multi.sh:38-82 starts one pod per rank; here one process
+per GPU on one node):
+* ``WORLD_SIZE`` set (torchrun / the driver): this process is one rank.
+* ``WORLD_SIZE`` unset and ``--gpus N > 1``: this process is only a launcher.  It never touches the
+  GPU; it starts ``torch.distributed.run`` with N ranks as a CHILD process (no exec), streams its
+  output (rank 0 prints the JSON line) and exits with the child's status, which is non-zero if any
+  rank failed.
+* ``--device cpu`` runs the same code on gloo / CPU (tests).  ``DLTB_COMM=host`` on a GPU makes
+  every rank use gloo with host-staged buffers, so N ranks can share one GPU (tests of the
+  multi-rank code paths on a one-GPU box; not a performance mode).
 
 K steps are timed between a barrier + torch.cuda.synchronize() on both sides; the time is the MAX over
 ranks; rank 0 prints one JSON line.  ``value`` is the whole-job tokens/s over all N GPUs.
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
 BASELINE_TPS = 18147.0   # BASELINE.md: best published (ZeRO-2 @ 4x A10), README.md:207,221
 BASELINES = {"ddp": {2: 8369.4557, 4: 12220.3415}, "fsdp": {2: 6771.0, 4: 9424.0},
              "zero2": {2: 10999.0, 4: 18147.0}, "zero3": {2: 10560.0, 4: 15977.0}}
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one per GPU)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--strategy", default="zero2", choices=["ddp", "fsdp", "zero2", "zero3"])
+    ap.add_argument("--tier", default="A")
+    ap.add_argument("--seq-len", type=int, default=2048)
+    ap.add_argument("--per-device-batch", type=int, default=1)
+    ap.add_argument("--grad-accum", type=int, default=4)
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="gradient bucket cap in MiB (default: comm.topology's measured/modelled choice)")
+    ap.add_argument("--accum-semantics", default="reference", choices=["reference", "uniform"])
+    ap.add_argument("--grad-reduce", default="micro", choices=["micro", "window"],
+                    help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed stage 2, default) or "
+                         "once per accumulation window (ZeRO-1 communication, reported as zero1-dpN)")
+    ap.add_argument("--grad-comm-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="DDP gradient all-reduce dtype (fp32 = the reference's torch DDP)")
+    ap.add_argument("--fsdp-wrap", default="block", choices=["block", "root"],
+                    help="FSDP unit layout: per transformer block, or the reference's single root FlatParameter")
+    ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
+                    help="replay each micro-step as a captured HIP graph (DLTB_GRAPHS overrides)")
+    ap.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
+                    help="hipBLASLt GEMM solutions from configs/tunableop (auto = use if present)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = gloo / CPU reference ops (tests of the launcher and the engines)")
+    ap.add_argument("--timeout-min", type=int, default=10, help="collective timeout")
+    ap.add_argument("--fail-rank", type=int, default=None, help="(tests) this rank raises before timing")
+    return ap
 
 
 def _model_name(tier, c):
@@ -39,133 +84,184 @@ def _model_name(tier, c):
     return f"TinyGPT-{tier} ({c.num_params() / 1e6:.1f}M params, d{c.n_embd}/h{c.n_head}/L{c.n_layer}, vocab {c.vocab_size})"
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--strategy", default="zero2", choices=["ddp", "fsdp", "zero2", "zero3"])
-    ap.add_argument("--tier", default="A")
-    ap.add_argument("--seq-len", type=int, default=2048)
-    ap.add_argument("--per-device-batch", type=int, default=1)
-    ap.add_argument("--grad-accum", type=int, default=4)
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--accum-semantics", default="reference", choices=["reference", "uniform"])
-    ap.add_argument("--grad-reduce", default="auto", choices=["auto", "micro", "window"],
-                    help="ZeRO-2 gradient reduce-scatter: every micro-step (DeepSpeed) or once per "
-                         "accumulation window; auto = window on N > 1 (xGMI is point-to-point: 1/4 "
-                         "of the traffic), no collective at all on N = 1")
-    ap.add_argument("--no-align", action="store_true", help="do not align warmup to accumulation windows")
-    ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
-                    help="replay each micro-step as a captured HIP graph (DLTB_GRAPHS overrides)")
-    ap.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
-                    help="hipBLASLt GEMM solutions from configs/tunableop (auto = use if present)")
-    args = ap.parse_args()
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    import dltb
+
+def launch(args, argv) -> int:
+    """Launcher mode: N ranks under torch.distributed.run as a child process.  Nothing here
+    initialises the GPU (no torch import at all), so the parent never holds a device context."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "--max-restarts=0",
+           os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    env["PYTHONUNBUFFERED"] = "1"
+    proc = subprocess.run(cmd, env=env, cwd=ROOT)
+    return proc.returncode
+
+
+def run_rank(args) -> int:
+    import torch
+    import dltb  # noqa: F401
     from dltb.data import SyntheticDataset, make_batcher
     from dltb.harness import _engine_for
     from dltb.models import build_model, get_model_config
-    from dltb.ops._ext import ext
     from dltb.parallel import GraphedStep, graphs_enabled
+    from dltb.comm.topology import recommend_bucket_mb
     from dltb.utils.dist import all_reduce_max, barrier, cleanup_distributed, setup_distributed
-    from dltb.utils.gemm_tuning import flush_tunableop, setup_tunableop
+    from dltb.utils.timers import PhaseTimers
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    device = setup_distributed(world, rank, local, device_type="cuda")
-    ext()   # fail loudly if the HIP extension is missing
-    tmode = setup_tunableop(args.tunableop if (args.tunableop != "tune" or rank == 0) else "use")
-    torch.manual_seed(42)
-    mcfg = get_model_config(args.tier, args.seq_len)
-    with torch.device(device):          # random init straight into HBM (7B-class models never touch host RAM)
-        model = build_model(mcfg)
-    grad_reduce = args.grad_reduce
-    if grad_reduce == "auto":
-        grad_reduce = "window" if (world > 1 and args.strategy == "zero2") else "micro"
-    h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None,
-                           grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype="bf16",
-                           bucket_mb=args.bucket_mb, seed=42, grad_reduce=grad_reduce)
-    engine, ecfg = _engine_for(h, model, device)
-    ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
-    batches = make_batcher("device", ds, args.per_device_batch, world, rank, args.strategy, device)
-    engine.train()
-    accum = engine.accum
-    warm = args.warmup
-    if not args.no_align and accum > 1:
-        warm = int(math.ceil(warm / accum) * accum)      # timed region starts at a window boundary
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    device = setup_distributed(world, rank, local, device_type=args.device, timeout_min=args.timeout_min)
+    cuda = device.type == "cuda"
+    try:
+        tmode = "off"
+        if cuda:
+            from dltb.ops._ext import ext
+            from dltb.utils.gemm_tuning import setup_tunableop
+            ext()   # fail loudly if the HIP extension is missing
+            tmode = setup_tunableop(args.tunableop if (args.tunableop != "tune" or rank == 0) else "use")
+        torch.manual_seed(42)
+        mcfg = get_model_config(args.tier, args.seq_len)
+        with torch.device(device):          # random init straight into HBM
+            model = build_model(mcfg)
+        bucket_mb = args.bucket_mb if args.bucket_mb is not None else recommend_bucket_mb(world)
+        h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None,
+                               grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype="bf16",
+                               bucket_mb=bucket_mb, seed=42, grad_reduce=args.grad_reduce,
+                               grad_comm_dtype=args.grad_comm_dtype, fsdp_wrap=args.fsdp_wrap)
+        engine, ecfg = _engine_for(h, model, device)
+        ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
+        batches = make_batcher("device", ds, args.per_device_batch, world, rank, args.strategy, device)
+        engine.train()
+        accum = engine.accum
+        use_graphs = graphs_enabled(args.graphs, device, world)
+        runner = GraphedStep(engine) if use_graphs else None
+        timers = PhaseTimers(device) if runner is None else None   # eager: exposed-comm time from HIP events
 
-    use_graphs = graphs_enabled(args.graphs, device, world)
-    runner = GraphedStep(engine) if use_graphs else None
+        def one_step(timed):
+            b = next(batches)
+            if runner is not None:
+                return runner(b, b)
+            if timed and timers is not None:
+                engine.timers = timers
+                timers.begin_step()
+            loss = engine(b, b)[1]
+            engine._phase("fwd_end")
+            engine.backward(loss)
+            engine._phase("bwd_end")
+            engine.step()
+            if timed and timers is not None:
+                timers.end_step()
+                engine.timers = None
+            return loss
 
-    def one_step():
-        b = next(batches)
-        if runner is not None:
-            return runner(b, b)
-        loss = engine(b, b)[1]
-        engine.backward(loss)
-        engine.step()
-        return loss
+        sync = (lambda: torch.cuda.synchronize(device)) if cuda else (lambda: None)
+        if cuda:
+            torch.cuda.reset_peak_memory_stats(device)
+        for _ in range(args.warmup):
+            loss = one_step(False)
+        if args.fail_rank is not None and rank == args.fail_rank:
+            raise RuntimeError(f"injected failure on rank {rank} (--fail-rank)")
+        opt0 = engine.opt_steps
+        loss_hist = torch.zeros(max(1, args.steps), dtype=torch.float32, device=device)
+        barrier()
+        sync()
+        engine.comm.reset_stats()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            loss = one_step(True)
+            loss_hist[i].copy_(loss.detach().reshape(()))   # a copy: graph replays reuse one loss tensor
+        barrier()
+        sync()
+        elapsed = all_reduce_max(time.perf_counter() - t0, device)
+        opt_steps = engine.opt_steps - opt0
+        engine.finalize()                    # a deferred update of the last window: outside the timed region
+        mean_loss = float(loss_hist[:args.steps].mean().item()) if args.steps else 0.0
+        final_loss = float(loss.item())
+        peak_gb = torch.cuda.max_memory_allocated(device) / 1e9 if cuda else 0.0
+        peak_gb = all_reduce_max(peak_gb, device)
+        phases = timers.summary() if timers is not None else None
+        comm_wait = all_reduce_max(phases["comm_wait"], device) if phases else 0.0
+        graphed = bool(runner is not None and runner.graphs and not runner.disabled)
+        wire = engine.comm.wire_bytes() / args.steps if (args.steps and not graphed) else None
+        ms = elapsed / max(1, args.steps) * 1e3
+        tokens = args.per_device_batch * args.seq_len * world * args.steps
+        value = tokens / elapsed if elapsed > 0 else 0.0
+        label = args.strategy
+        if args.strategy == "zero2" and ecfg.zero_stage == 1:
+            label = "zero1"                  # window-reduced: ZeRO-1 communication
+        if args.strategy == "fsdp" and ecfg.wrap == "root":
+            label = "fsdp_root"
+        if rank == 0:
+            flops = mcfg.train_flops_per_token(args.seq_len)
+            same = BASELINES.get(args.strategy) if label == args.strategy else None
+            out = {
+                "metric": "tokens_per_sec",
+                "value": value,
+                "unit": "tokens/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": ms,
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": value / BASELINE_TPS if (args.tier == "A" and args.seq_len == 2048) else None,
+                "dtype": "bf16" if cuda else "fp32",
+                "data": "synthetic tokens (fixed random table, seed 42), random-init weights",
+                "config": {"model": _model_name(args.tier, mcfg),
+                           "global_batch": args.per_device_batch * accum * world,
+                           "micro_batch_per_gpu": args.per_device_batch,
+                           "grad_accum": accum,
+                           "seq_len": args.seq_len,
+                           "parallelism": f"{label}-dp{world}",
+                           "grad_reduce": ecfg.extra.get("grad_reduce"),
+                           "grad_comm_dtype": args.grad_comm_dtype if args.strategy == "ddp" else None,
+                           "bucket_mb": bucket_mb},
+                "strategy": args.strategy,
+                "world_size_seen": engine.comm.world,
+                "backend": engine.comm.backend,
+                "warmup_requested": args.warmup,
+                "warmup_used": args.warmup,
+                "optimizer_steps_timed": opt_steps,
+                "mean_loss": mean_loss,
+                "final_loss": final_loss,
+                "peak_hbm_gb": peak_gb,
+                "comm_wait_ms": comm_wait if phases else None,
+                "phase_ms": phases,
+                "wire_bytes_per_step": wire,
+                "wire_bytes_per_step_model": engine.comm_bytes_per_step,
+                "tflops_per_gpu": value / world * flops / 1e12,
+                "mfu_dense_bf16": value / world * flops / 2.5e15,
+                "baseline_note": "vs_baseline = value / 18147 tok/s (reference best: ZeRO-2 on 4x A10, BASELINE.md)",
+                "same_strategy_published": same,
+                "gemm_tuning": tmode,
+                "hip_graphs": graphed,
+            }
+            print(json.dumps(out), flush=True)
+        if cuda:
+            from dltb.utils.gemm_tuning import flush_tunableop
+            flush_tunableop()
+        return 0
+    finally:
+        cleanup_distributed()
 
-    torch.cuda.reset_peak_memory_stats(device)
-    for _ in range(warm):
-        loss = one_step()
-    opt0 = engine.opt_steps
-    barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = one_step()
-    barrier()
-    torch.cuda.synchronize(device)
-    elapsed = all_reduce_max(time.perf_counter() - t0, device)
-    opt_steps = engine.opt_steps - opt0
-    final_loss = float(loss.item())
-    peak_gb = torch.cuda.max_memory_allocated(device) / 1e9
-    peak_gb = all_reduce_max(peak_gb, device)
-    ms = elapsed / args.steps * 1e3
-    tokens = args.per_device_batch * args.seq_len * world * args.steps
-    value = tokens / elapsed
-    if rank == 0:
-        flops = mcfg.train_flops_per_token(args.seq_len)
-        out = {
-            "metric": "tokens_per_sec",
-            "value": value,
-            "unit": "tokens/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": warm,
-            "ms_per_step": ms,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": value / BASELINE_TPS if (args.tier == "A" and args.seq_len == 2048) else None,
-            "dtype": "bf16",
-            "data": "synthetic",
-            "config": {"model": _model_name(args.tier, mcfg),
-                       "global_batch": args.per_device_batch * accum * world,
-                       "micro_batch_per_gpu": args.per_device_batch,
-                       "grad_accum": accum,
-                       "seq_len": args.seq_len,
-                       "parallelism": f"{args.strategy}-dp{world}",
-                       "grad_reduce": grad_reduce if args.strategy == "zero2" else None},
-            "strategy": args.strategy,
-            "optimizer_steps_timed": opt_steps,
-            "peak_hbm_gb": peak_gb,
-            "tflops_per_gpu": value / world * flops / 1e12,
-            "mfu_dense_bf16": value / world * flops / 2.5e15,
-            "final_loss": final_loss,
-            "baseline_note": "vs_baseline = value / 18147 tok/s (reference best: ZeRO-2 on 4x A10, BASELINE.md)",
-            "same_strategy_published": BASELINES.get(args.strategy),
-            "gemm_tuning": tmode,
-            "hip_graphs": use_graphs,
-        }
-        print(json.dumps(out), flush=True)
-    flush_tunableop()
-    cleanup_distributed()
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = build_parser().parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch(args, argv)
+    return run_rank(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -15,6 +15,14 @@ engines own their communication, and this module is the one place that talks to
   step actually moved over xGMI, per op.
 * ``world == 1``: every op is a no-op that returns a completed work, so engines need no
   single-process special cases around their collectives.
+* Host-staged mode (gloo process group, device tensors; ``DLTB_COMM=host`` in
+  ``utils.dist.setup_distributed``): every collective copies its device buffer to host memory,
+  runs the gloo op there (bf16 / fp16 / fp32 are all supported) and copies the result back,
+  synchronously.  RCCL refuses two ranks on one GPU; this mode lets N ranks share the single
+  MI355X of a test box, so every code path that exists only at world > 1 (bf16 flat buckets, the
+  per-bucket batched weight gradients, deferred all-gathers waited in ``acquire``, fp32
+  accumulation of reduce-scattered chunks, ZeRO-3 transient gather buffers) runs with the real
+  HIP kernels.  It is a correctness mode, not a performance mode.
 """
 from collections import OrderedDict
 
@@ -53,6 +61,7 @@ class Comm:
         self.world = dist.get_world_size(group) if self.enabled else 1
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.backend = dist.get_backend(group) if self.enabled else "none"
+        self.staged = self.backend == "gloo"      # device tensors go through host memory
         self._pending = []
         self.stats = OrderedDict()            # op -> {"calls": n, "wire_bytes": b}
 
@@ -87,12 +96,25 @@ class Comm:
     def pending(self) -> int:
         return len(self._pending)
 
+    # ------------------------------------------------------------------ host staging (gloo)
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        return t.to("cpu") if t.is_cuda else t
+
+    def _back(self, dst: torch.Tensor, h: torch.Tensor):
+        if dst.data_ptr() != h.data_ptr() or dst.device != h.device:
+            dst.copy_(h)
+
     # ------------------------------------------------------------------ collectives
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = True, track: bool = True):
         """In-place all-reduce of a flat buffer slice (DDP bucket, grad-norm scalar)."""
         if self.world == 1:
             return _DONE
         self._count("all_reduce", t)
+        if self.staged and t.is_cuda:
+            h = self._host(t)
+            dist.all_reduce(h, op=getattr(dist.ReduceOp, _REDUCE_OPS[op]), group=self.group)
+            self._back(t, h)
+            return _DONE
         w = dist.all_reduce(t, op=getattr(dist.ReduceOp, _REDUCE_OPS[op]), group=self.group,
                             async_op=async_op)
         return self._track(w, async_op) if track else (w if async_op else _DONE)
@@ -106,6 +128,11 @@ class Comm:
             return _DONE
         assert inp.numel() == out.numel() * self.world, "reduce_scatter: input must be world x output"
         self._count("reduce_scatter", inp)
+        if self.staged and (inp.is_cuda or out.is_cuda):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.reduce_scatter_tensor(h, self._host(inp), group=self.group)
+            self._back(out, h)
+            return _DONE
         w = dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
         return self._track(w, async_op) if track else (w if async_op else _DONE)
 
@@ -119,6 +146,11 @@ class Comm:
             return _DONE
         assert out.numel() == inp.numel() * self.world, "all_gather: output must be world x input"
         self._count("all_gather", out)
+        if self.staged and (inp.is_cuda or out.is_cuda):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(h, self._host(inp), group=self.group)
+            self._back(out, h)
+            return _DONE
         w = dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
         return self._track(w, async_op) if track else (w if async_op else _DONE)
 
@@ -126,6 +158,11 @@ class Comm:
         if self.world == 1:
             return
         self._count("broadcast", t)
+        if self.staged and t.is_cuda:
+            h = self._host(t)
+            dist.broadcast(h, src=src, group=self.group)
+            self._back(t, h)
+            return
         dist.broadcast(t, src=src, group=self.group)
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
@@ -133,6 +170,11 @@ class Comm:
             out.copy_(inp)
             return _DONE
         self._count("all_to_all", inp)
+        if self.staged and (inp.is_cuda or out.is_cuda):
+            h = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(h, self._host(inp), group=self.group)
+            self._back(out, h)
+            return _DONE
         w = dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
         return self._track(w, async_op)
 
@@ -144,6 +186,6 @@ class Comm:
         """Host float max over ranks (timings, peak memory)."""
         if self.world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=device)
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if self.staged else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())

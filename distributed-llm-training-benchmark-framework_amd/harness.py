@@ -69,6 +69,8 @@ def build_parser():
     p.add_argument("--grad-reduce", choices=["micro", "window"], default="micro",
                    help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed) or once per "
                         "accumulation window")
+    p.add_argument("--grad-comm-dtype", choices=["bf16", "fp32"], default="bf16",
+                   help="DDP gradient all-reduce dtype (fp32 = the reference's torch DDP)")
     p.add_argument("--dtype", choices=list(DTYPES), default="bf16")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda" if torch.cuda.is_available() else "cpu")
     p.add_argument("--bucket-mb", type=float, default=64.0, help="gradient bucket cap (MiB)")
@@ -107,9 +109,12 @@ def _engine_for(args, model, device):
         path = args.fsdp_config or default_config_path("fsdp")
         if path and os.path.exists(path):
             fc = load_fsdp_config(path)
+        if getattr(args, "fsdp_wrap", None) == "root":      # the reference's single root FlatParameter
+            fc = dict(fc or {}, auto_wrap_policy="size_based")
     cfg = engine_config(args.strategy, args.grad_accum, args.accum_semantics, ds, fc,
                         compute_dtype=DTYPES[args.dtype], bucket_mb=args.bucket_mb, seed=args.seed,
                         grad_reduce=getattr(args, "grad_reduce", "micro"))
+    cfg.extra["grad_comm_dtype"] = getattr(args, "grad_comm_dtype", "bf16")
     return make_engine(model, cfg, device), cfg
 
 
@@ -158,11 +163,16 @@ def train(args):
         runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device, world) and not args.profile
                                          and not args.phase_timers) else None
         timers = PhaseTimers(device) if args.phase_timers else None
-        losses = []
+        timed_n = max(0, args.steps - args.warmup_steps)
+        # per-step losses are COPIED into a device buffer: a graph replay returns the same static
+        # loss tensor for every replay of a window position, so keeping the tensors would alias
+        loss_hist = torch.zeros(max(1, timed_n), dtype=torch.float32, device=device)
+        n_loss = 0
         step_events = []
         host_times = []
         prof = None
         t_start = None
+        t_log = [time.perf_counter(), 0]
         sync = (lambda: torch.cuda.synchronize(device)) if device.type == "cuda" else (lambda: None)
         for step in range(args.steps):
             if step == args.warmup_steps:
@@ -206,7 +216,8 @@ def train(args):
                 ev1.record()
                 step_events.append((ev0, ev1))
             if step >= args.warmup_steps:
-                losses.append(loss.detach())
+                loss_hist[n_loss].copy_(loss.detach().reshape(()))
+                n_loss += 1
                 host_times.append(h1 - h0)
             if prof is not None and step >= args.warmup_steps + args.profile_steps - 1:
                 sync()
@@ -215,9 +226,17 @@ def train(args):
                 prof.export_chrome_trace(os.path.join(args.profile, f"trace_{args.strategy}_ws{world}_rank{rank}.json"))
                 prof = None
             if is_main and args.log_every and step % args.log_every == 0:
-                print(f"[Step {step:04d}] Loss: {loss.item():.4f}, Time: {h1 - h0:.3f}s", flush=True)
+                lv = loss.item()             # synchronises: Time is the mean device-synchronised
+                now = time.perf_counter()    # step time since the previous log line
+                dt = (now - t_log[0]) / max(1, step - t_log[1]) if step > 0 else h1 - h0
+                t_log[:] = [now, step]
+                print(f"[Step {step:04d}] Loss: {lv:.4f}, Time: {dt:.4f}s", flush=True)
         barrier()
         sync()
+        timed = args.steps - args.warmup_steps
+        # the timed region ends here: finalize / checkpoint / export below are not step time
+        wall = (time.perf_counter() - t_start) if (t_start is not None and timed > 0) else 0.0
+        wall = all_reduce_max(wall, device)
         engine.finalize()            # a deferred optimizer step of the last window (outside the timed region)
         if args.save_dir:
             if engine.micro % engine.accum == 0:
@@ -228,11 +247,8 @@ def train(args):
                 print("WARNING: --save-dir skipped: the run did not end on an accumulation boundary", flush=True)
         if args.export_model:
             export_consolidated(engine, args.export_model)
-        timed = args.steps - args.warmup_steps
-        wall = (time.perf_counter() - t_start) if (t_start is not None and timed > 0) else 0.0
-        wall = all_reduce_max(wall, device)
         mean_step = wall / timed if timed > 0 else 0.0
-        mean_loss = torch.stack(losses).float().mean().item() if losses else 0.0
+        mean_loss = float(loss_hist[:n_loss].mean().item()) if n_loss else 0.0
         peak = torch.cuda.max_memory_allocated(device) if device.type == "cuda" else 0
         record = make_record(args.strategy, world, rank, args.seq_len, args.tier, args.steps,
                              args.per_device_batch, args.grad_accum, mean_step, mean_loss, peak)
@@ -265,7 +281,8 @@ def train(args):
             "comm_topology": comm_describe(world) if (is_main and device.type == "cuda") else None,
             "memory": engine.memory_report(),
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
-            "accum_semantics": args.accum_semantics, "grad_reduce": args.grad_reduce, "dtype": args.dtype, "data_loader": args.data_loader,
+            "accum_semantics": args.accum_semantics, "grad_reduce": args.grad_reduce, "dtype": args.dtype,
+            "grad_comm_dtype": args.grad_comm_dtype, "data_loader": args.data_loader,
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
             "phase_times_ms": timers.summary() if timers is not None else None,
         }

@@ -15,8 +15,13 @@ accumulate, the last also runs clipping + fused AdamW + parameter all-gather) in
 Everything inside a captured region reads step-dependent values from device memory: the dropout
 seed (``StepSeed.device_tensor``), AdamW's lr / bias corrections (``FlatAdamW.hp``), the clip
 coefficient (computed on the device).  Graphs share one memory pool and are replayed in capture
-order.  Capture happens on the first window after an eager warm-up window (hipBLASLt handles,
-TunableOp lookups, allocator pools and lazily built tables exist by then).  Collectives (RCCL
+order.  Capture happens at the start of the first window after an eager warm-up window
+(hipBLASLt handles, TunableOp lookups, allocator pools and lazily built tables exist by then):
+all ``accum`` positions are captured back to back -- a capture runs no GPU work, it only
+advances the host bookkeeping -- then the host state is rewound and position 0 is replayed.  A
+run therefore replays from its ``accum + 1``-th micro-step on, so a short warm-up (bench.py's
+``--warmup 5`` at grad-accum 4) keeps every capture out of the timed region.  The loss returned
+by a replay is the graph's static output tensor: callers that keep per-step losses copy it.  Collectives (RCCL
 reduce-scatter / all-gather / all-reduce on the process group's stream) are captured with the
 rest; ``DLTB_GRAPHS=0`` or ``--graphs off`` restores eager execution.
 """
@@ -67,38 +72,44 @@ class GraphedStep:
         self.n += 1
         if self.disabled or self.n <= self.capture_after or (not self.graphs and pos != 0):
             return self._eager(idx, tgt)            # warm-up, then start capturing at a window start
-        if pos in self.graphs:
-            g, loss = self.graphs[pos]
-            e.replay_host_step()
-            self.static_idx.copy_(idx)
-            if tgt is not idx:
-                self.static_tgt.copy_(tgt)
-            g.replay()
-            return loss
+        if not self.graphs and not self._capture_window(idx, tgt):
+            return self._eager(idx, tgt)
+        g, loss = self.graphs[pos]
+        e.replay_host_step()
+        self.static_idx.copy_(idx)
+        if tgt is not idx:
+            self.static_tgt.copy_(tgt)
+        g.replay()
+        return loss
+
+    def _capture_window(self, idx, tgt) -> bool:
+        """Capture one graph per window position (called at a window start).  Returns False (and
+        disables graphs for good) when a capture fails; the host state is rewound either way."""
         if self.static_idx is None:
             self.static_idx = idx.clone()
             self.static_tgt = self.static_idx if tgt is idx else tgt.clone()
-        self.static_idx.copy_(idx)
-        if self.static_tgt is not self.static_idx:
-            self.static_tgt.copy_(tgt)
         torch.cuda.synchronize()
         snap = self._host_state()
-        g = torch.cuda.CUDAGraph()
+        graphs = {}
         try:
-            # thread_local: the process group's watchdog thread may query events meanwhile
-            with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
-                loss = self._eager(self.static_idx, self.static_tgt)
+            for k in range(self.accum):
+                g = torch.cuda.CUDAGraph()
+                # thread_local: the process group's watchdog thread may query events meanwhile
+                with torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local"):
+                    loss = self._eager(self.static_idx, self.static_tgt)
+                self.pool = g.pool()
+                graphs[k] = (g, loss)
         except Exception as exc:  # noqa: BLE001 - fall back to eager execution for good
             self._restore_host_state(snap)
             self.disabled = True
             print(f"[dltb] HIP-graph capture failed ({type(exc).__name__}: {exc}); running eagerly", flush=True)
             torch.cuda.synchronize()
-            return self._eager(idx, tgt)
-        self.pool = g.pool()
-        e.upload_step_state()
-        g.replay()
-        self.graphs[pos] = (g, loss)
-        return loss
+            return False
+        self._restore_host_state(snap)       # the captures ran no GPU work: replay from position 0
+        if self.e.opt.step_count > 0:
+            self.e.opt.upload()
+        self.graphs = graphs
+        return True
 
     def _host_state(self):
         e = self.e

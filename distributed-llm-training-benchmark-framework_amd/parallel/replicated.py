@@ -59,6 +59,14 @@ class ReplicatedEngine(Engine):
             master_full[s.offset:s.offset + s.numel] = p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
         self.flat_param = master_full.to(dt)
         self.flat_grad = torch.zeros(L.total, dtype=dt, device=dev)
+        # DDP all-reduce dtype.  bf16: the flat gradient buffer itself is reduced.  fp32: what the
+        # reference's torch DDP reduces (fp32 grads under fp16 autocast, train_harness.py:217-222):
+        # each bucket is widened into an fp32 buffer right before its all-reduce, summed over the
+        # ranks in fp32, and AdamW reads the fp32 sum (2x the wire bytes, no bf16 rounding per hop)
+        self.comm_f32 = None
+        if self.stage == 0 and self.world > 1 and cfg.extra.get("grad_comm_dtype") == "fp32" \
+                and dt != torch.float32:
+            self.comm_f32 = torch.zeros(L.total, dtype=torch.float32, device=dev)
         for s in L.slots.values():
             p = s.unit.params[s.index]
             p.data = self.flat_param[s.offset:s.offset + s.numel].view(s.shape)
@@ -114,10 +122,17 @@ class ReplicatedEngine(Engine):
         self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda" and bool(
             cfg.extra.get("shared_colreduce", os.environ.get("DLTB_SHARED_COLREDUCE", "1") == "1"))) else None
         self._launched = [False] * len(L.buckets)
-        nbytes = L.total * elem
+        nbytes = L.total * (4 if self.comm_f32 is not None else elem)
         if self.world > 1:
-            ring = 2 * (self.world - 1) / self.world
-            self.comm_bytes_per_step = int(nbytes * (ring if self.stage == 0 else ring / 2))
+            # modelled wire bytes one rank sends per micro-step (ring algorithms): DDP one all-reduce
+            # per optimizer step; ZeRO-2 a reduce-scatter every micro-step; ZeRO-1 one per window;
+            # ZeRO-1/2 also one parameter all-gather per window
+            frac = (self.world - 1) / self.world
+            if self.stage == 0:
+                per = 2 * frac * nbytes / self.accum
+            else:
+                per = frac * nbytes * (1.0 if self.stage == 2 else 1.0 / self.accum) + frac * nbytes / self.accum
+            self.comm_bytes_per_step = int(per)
 
     # ------------------------------------------------------------------ runtime interface
     def weight_t(self, unit, i, w):
@@ -213,7 +228,15 @@ class ReplicatedEngine(Engine):
         bk = self.layout.buckets[b]
         g = self.flat_grad[bk.start:bk.end]
         if self.stage == 0:
-            self.comm.all_reduce(g)
+            if self.comm_f32 is not None:
+                c = self.comm_f32[bk.start:bk.end]
+                if c.is_cuda:
+                    ext().f32_from_bf16_(c, g, False)
+                else:
+                    c.copy_(g)
+                self.comm.all_reduce(c)
+            else:
+                self.comm.all_reduce(g)
         else:
             self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g)
         self._launched[b] = True
@@ -249,7 +272,7 @@ class ReplicatedEngine(Engine):
 
     def _owner_grad(self):
         if self.stage == 0:
-            return self.flat_grad
+            return self.comm_f32 if self.comm_f32 is not None else self.flat_grad
         if self.acc is not None and self.stage == 2:
             return self.acc
         return self.rs_out if self.world > 1 else self.flat_grad

@@ -290,8 +290,11 @@ class ShardedEngine(Engine):
         g = self._group_of[id(unit)]
         if any(self._persistent(unit, i) for i in range(len(unit.params))):
             self._p_left -= 1
-            if self._p_left == 0:
+            if self._p_left == 0 and self.world > 1:
                 self._reduce_persistent()
+            # (world 1: the persistent slots are final only after the batched dW flush -- a 2-D
+            # parameter below the persistence threshold gets its gradient from the queue -- so
+            # they are handed to the owner space in _finish_backward)
         g.bwd_left -= 1
         if g.bwd_left == 0:
             self._reduce_group(g)
@@ -330,7 +333,7 @@ class ShardedEngine(Engine):
     def _finish_backward(self):
         self._wq.flush()
         if self._p_left != self._p_pending:      # persistent params of units that never reported
-            if self._p_left > 0:
+            if self._p_left > 0 or self.world == 1:
                 self._reduce_persistent()
             self._p_left = self._p_pending
         for g in self.groups:                     # groups whose backward did not run fully

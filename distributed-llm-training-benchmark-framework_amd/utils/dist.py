@@ -31,9 +31,12 @@ def resolve_ranks(world_size=None, rank=None, local_rank=None):
 def setup_distributed(world_size, rank, local_rank, master_addr=None, master_port=None,
                       device_type="cuda", timeout_min=30, debug_collectives=False):
     """Initialise the process group when world_size > 1; returns the torch.device of this rank."""
+    host_comm = device_type == "cuda" and os.environ.get("DLTB_COMM", "rccl") == "host"
     if device_type == "cuda":
         if not torch.cuda.is_available():
             raise RuntimeError("no GPU visible (use --device cpu for the gloo/CPU path)")
+        if host_comm:     # ranks may outnumber the GPUs: they share them round-robin
+            local_rank = local_rank % torch.cuda.device_count()
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
     else:
@@ -47,10 +50,12 @@ def setup_distributed(world_size, rank, local_rank, master_addr=None, master_por
             os.environ.setdefault("MASTER_PORT", str(master_port))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        # DLTB_COMM=host: gloo with host-staged device buffers (comm/collectives.py), so several
+        # ranks can share one GPU (tests of the world > 1 paths on a one-GPU box)
+        backend = "nccl" if (device_type == "cuda" and not host_comm) else "gloo"
         kw = dict(backend=backend, init_method="env://", world_size=world_size, rank=rank,
                   timeout=datetime.timedelta(minutes=timeout_min))
-        if device_type == "cuda":
+        if backend == "nccl":
             kw["device_id"] = device
             if os.environ.get("DLTB_COMM_HIGH_PRIORITY", "1") == "1":
                 # RCCL's internal stream at high priority: when bucket collectives and backward
@@ -60,7 +65,7 @@ def setup_distributed(world_size, rank, local_rank, master_addr=None, master_por
                 opts.is_high_priority_stream = True
                 kw["pg_options"] = opts
         dist.init_process_group(**kw)
-        if device_type == "cuda":      # warm the communicator up outside the timed region
+        if backend == "nccl":          # warm the communicator up outside the timed region
             t = torch.ones(1, device=device)
             dist.all_reduce(t)
             torch.cuda.synchronize(device)
@@ -83,7 +88,8 @@ def barrier():
 
 def all_reduce_max(x: float, device) -> float:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        t = torch.tensor([x], dtype=torch.float64, device=device)
+        host = dist.get_backend() == "gloo"
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if host else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
     return x

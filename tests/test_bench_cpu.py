@@ -1,0 +1,68 @@
+"""bench.py launcher contract on CPU / gloo (the GPU path runs the same code with RCCL).
+
+* ``python bench.py --gpus 2`` without a torchrun environment starts the ranks itself as a child
+  ``torch.distributed.run`` (reference: scripts/launch_multi.sh:38-82 starts one pod per rank),
+  and exactly one JSON line comes back with n_gpus == world_size_seen == 2.
+* A failing rank makes the launcher exit non-zero.
+* Exactly ``--warmup`` untimed steps and ``--steps`` timed steps: the record says so.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BASE = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--tier", "tiny",
+        "--seq-len", "64", "--steps", "8", "--warmup", "5"]
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def _json_lines(out):
+    return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+
+
+def test_bench_self_launch_two_ranks():
+    r = subprocess.run(BASE + ["--gpus", "2"], capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == rec["world_size_seen"] == 2
+    assert rec["backend"] == "gloo"
+    assert rec["steps"] == 8 and rec["warmup"] == 5 == rec["warmup_used"] == rec["warmup_requested"]
+    assert rec["config"]["parallelism"] == "zero2-dp2" and rec["config"]["grad_reduce"] == "micro"
+    assert rec["optimizer_steps_timed"] == 2          # any 8 consecutive micro-steps hold 2 boundaries
+    # ZeRO-2: a reduce-scatter every micro-step + the window's all-gather, measured == modelled
+    assert rec["wire_bytes_per_step"] > 0
+    assert abs(rec["wire_bytes_per_step"] - rec["wire_bytes_per_step_model"]) / rec["wire_bytes_per_step_model"] < 0.01
+    assert rec["comm_wait_ms"] is not None and rec["mean_loss"] > 0
+
+
+def test_bench_window_is_labelled_zero1():
+    r = subprocess.run(BASE + ["--gpus", "2", "--grad-reduce", "window", "--steps", "4", "--warmup", "1"],
+                       capture_output=True, text=True, env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["config"]["parallelism"] == "zero1-dp2"
+    assert rec["same_strategy_published"] is None
+
+
+def test_bench_failing_rank_fails_the_launch():
+    r = subprocess.run(BASE + ["--gpus", "2", "--fail-rank", "1"], capture_output=True, text=True,
+                       env=_env(), timeout=600)
+    assert r.returncode != 0
+    assert not _json_lines(r.stdout)
+
+
+def test_bench_single_process_cpu():
+    r = subprocess.run(BASE + ["--gpus", "1", "--strategy", "ddp"], capture_output=True, text=True,
+                       env=_env(), timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["n_gpus"] == rec["world_size_seen"] == 1 and rec["wire_bytes_per_step"] == 0

@@ -1,0 +1,20 @@
+"""Multi-rank code paths on one MI355X: two ranks share cuda:0 (``DLTB_COMM=host``: gloo with
+host-staged device buffers, comm/collectives.py) and train every engine -- DDP (bf16 and fp32
+all-reduce), ZeRO-2 (per-micro-step and per-window reduce-scatter), ZeRO-3 (release + re-gather,
+persistent small params), FSDP per-block and root, Mistral-shape GQA under ZeRO-3 -- with the bf16
+HIP kernels, batched weight gradients per bucket, deferred all-gathers and fp32 accumulation of
+reduce-scattered chunks.  After 3 windows the parameter updates must match the world-1 GPU run on
+the concatenated batch within bf16 tolerance (reference: train_harness.py:210-271)."""
+import pytest
+
+from multirank_util import compare, run
+
+pytestmark = pytest.mark.gpu
+
+
+def test_world2_host_staged_equals_world1_gpu(tmp_path):
+    ws1 = run(tmp_path / "ws1.pt", 1, "cuda", timeout=600)
+    ws2 = run(tmp_path / "ws2.pt", 2, "cuda", env_extra={"DLTB_COMM": "host"}, timeout=600)
+    assert set(ws1) == set(ws2)
+    bad = compare(ws1, ws2, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
+    assert not bad, bad
