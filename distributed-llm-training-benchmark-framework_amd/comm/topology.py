@@ -12,6 +12,7 @@ a target fraction of its transfer time, so overlap with backward starts early wi
 launch latencies.  The reference's DDP uses 25 MiB buckets (NVSwitch/PCIe tuned) and DeepSpeed a
 single 5e8-element bucket.
 """
+import json
 import os
 import re
 import shutil
@@ -32,12 +33,67 @@ def collective_time_us(op: str, nbytes: int, world: int, bus_gbps: float = DEFAU
     return alpha_us + nbytes * ring_factor(op, world) / (bus_gbps * 1e3)
 
 
-def recommend_bucket_mb(world: int, overhead: float = 0.2, bus_gbps: float = DEFAULT_BUS_GBPS,
-                        alpha_us: float = DEFAULT_ALPHA_US, op: str = "reduce_scatter") -> float:
-    """Smallest power-of-two MiB bucket with alpha <= overhead x transfer time."""
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+DEFAULT_PROFILE = os.path.join(_ROOT, "profiles", "xgmi_buckets.json")
+
+
+def load_profile(path: str = None):
+    """The measured collective sweep written by scripts/run_all_benchmarks.sh (scripts/
+    bench_collectives.py at each world size): {"worlds": {"8": [row, ...]}} with rows
+    {"op", "bytes", "time_us", ...}.  ``$DLTB_XGMI_PROFILE`` overrides the default
+    ``profiles/xgmi_buckets.json``; None when absent or unreadable."""
+    path = path or os.environ.get("DLTB_XGMI_PROFILE") or DEFAULT_PROFILE
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        return data if isinstance(data.get("worlds"), dict) else None
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
+def fit_alpha_beta(rows, op: str, world: int):
+    """Least-squares fit time_us = alpha + bytes * ring_factor / (bus_GBps * 1e3) over the measured
+    sizes of ``op``; returns (alpha_us, bus_GBps) or None (fewer than 2 sizes, non-physical fit)."""
+    from .collectives import ring_factor
+    pts = [(float(r["bytes"]), float(r["time_us"])) for r in rows if r.get("op") == op]
+    if len(pts) < 2:
+        return None
+    n = len(pts)
+    mx = sum(x for x, _ in pts) / n
+    my = sum(y for _, y in pts) / n
+    sxx = sum((x - mx) ** 2 for x, _ in pts)
+    if sxx <= 0:
+        return None
+    slope = sum((x - mx) * (y - my) for x, y in pts) / sxx        # us per byte
+    alpha = my - slope * mx
+    f = ring_factor(op, world)
+    if slope <= 0 or f <= 0:
+        return None
+    return max(alpha, 1.0), f / (slope * 1e3)
+
+
+def measured_params(world: int, op: str = "reduce_scatter", path: str = None):
+    """(alpha_us, bus_GBps, source) for ``world`` ranks: the fit of the measured sweep when the
+    profile holds this world size, else the conservative defaults."""
+    prof = load_profile(path)
+    rows = (prof or {}).get("worlds", {}).get(str(world)) if prof else None
+    fit = fit_alpha_beta(rows, op, world) if rows else None
+    if fit is not None:
+        return fit[0], fit[1], "measured"
+    return DEFAULT_ALPHA_US, DEFAULT_BUS_GBPS, "default"
+
+
+def recommend_bucket_mb(world: int, overhead: float = 0.2, bus_gbps: float = None,
+                        alpha_us: float = None, op: str = "reduce_scatter") -> float:
+    """Smallest power-of-two MiB bucket with alpha <= overhead x transfer time, alpha and bus
+    bandwidth from the measured sweep (``load_profile``) when it covers ``world``."""
     from .collectives import ring_factor
     if world <= 1:
         return 64.0
+    if bus_gbps is None or alpha_us is None:
+        a, b, _ = measured_params(world, op)
+        alpha_us = a if alpha_us is None else alpha_us
+        bus_gbps = b if bus_gbps is None else bus_gbps
     f = ring_factor(op, world)
     need = alpha_us / overhead * bus_gbps * 1e3 / f       # bytes
     mb = 1.0
@@ -77,6 +133,8 @@ def describe(world: int) -> dict:
     """Summary used in result sidecars and docs."""
     topo = query_topology()
     xgmi = sum(1 for v in (topo or {}).values() if v == "XGMI")
+    alpha, bus, src = measured_params(world)
     return {"world": world, "xgmi_pairs": xgmi if topo else None,
             "links_per_gpu": XGMI_LINKS_PER_GPU, "link_GBps": XGMI_LINK_GBPS,
+            "alpha_us": alpha, "bus_GBps": bus, "alpha_beta_source": src,
             "recommended_bucket_mb": recommend_bucket_mb(world)}

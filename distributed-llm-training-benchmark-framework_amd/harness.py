@@ -73,7 +73,12 @@ def build_parser():
                    help="DDP gradient all-reduce dtype (fp32 = the reference's torch DDP)")
     p.add_argument("--dtype", choices=list(DTYPES), default="bf16")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda" if torch.cuda.is_available() else "cpu")
-    p.add_argument("--bucket-mb", type=float, default=64.0, help="gradient bucket cap (MiB)")
+    p.add_argument("--bucket-mb", type=float, default=None,
+                   help="gradient bucket cap (MiB); default: comm.topology.recommend_bucket_mb(world), "
+                        "from the measured xGMI sweep (profiles/xgmi_buckets.json) when present")
+    p.add_argument("--strategy-label", type=str, default=None,
+                   help="name of this run in the result record / file name / CSV (e.g. fsdp_root, "
+                        "ddp_uniform); default: --strategy")
     p.add_argument("--dropout", type=float, default=None, help="override the model dropout (reference: 0.1)")
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--data-loader", choices=["device", "host"], default="device")
@@ -121,6 +126,10 @@ def _engine_for(args, model, device):
 def train(args):
     world, rank, local_rank = resolve_ranks(args.world_size, args.rank, args.local_rank)
     args.world_size, args.rank, args.local_rank = world, rank, local_rank
+    if args.bucket_mb is None:
+        from .comm.topology import recommend_bucket_mb
+        args.bucket_mb = recommend_bucket_mb(world)
+    label = args.strategy_label or args.strategy
     device = setup_distributed(world, rank, local_rank, args.master_addr, args.master_port, args.device,
                                args.timeout_min, args.debug_collectives)
     is_main = rank == 0
@@ -223,7 +232,7 @@ def train(args):
                 sync()
                 prof.__exit__(None, None, None)
                 os.makedirs(args.profile, exist_ok=True)
-                prof.export_chrome_trace(os.path.join(args.profile, f"trace_{args.strategy}_ws{world}_rank{rank}.json"))
+                prof.export_chrome_trace(os.path.join(args.profile, f"trace_{label}_ws{world}_rank{rank}.json"))
                 prof = None
             if is_main and args.log_every and step % args.log_every == 0:
                 lv = loss.item()             # synchronises: Time is the mean device-synchronised
@@ -250,7 +259,7 @@ def train(args):
         mean_step = wall / timed if timed > 0 else 0.0
         mean_loss = float(loss_hist[:n_loss].mean().item()) if n_loss else 0.0
         peak = torch.cuda.max_memory_allocated(device) if device.type == "cuda" else 0
-        record = make_record(args.strategy, world, rank, args.seq_len, args.tier, args.steps,
+        record = make_record(label, world, rank, args.seq_len, args.tier, args.steps,
                              args.per_device_batch, args.grad_accum, mean_step, mean_loss, peak)
         ev_times = [a.elapsed_time(b) / 1e3 for a, b in step_events] if step_events else []
         tokens_step = args.per_device_batch * args.seq_len * world
@@ -282,7 +291,7 @@ def train(args):
             "memory": engine.memory_report(),
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
             "accum_semantics": args.accum_semantics, "grad_reduce": args.grad_reduce, "dtype": args.dtype,
-            "grad_comm_dtype": args.grad_comm_dtype, "data_loader": args.data_loader,
+            "grad_comm_dtype": args.grad_comm_dtype, "strategy_engine": args.strategy, "bucket_mb": args.bucket_mb, "data_loader": args.data_loader,
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
             "phase_times_ms": timers.summary() if timers is not None else None,
         }

@@ -22,7 +22,12 @@ DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
   point-to-point, so a ring reduce-scatter is per-link bound, and one reduce-scatter per window
   moves 1/grad_accum of the per-micro-step traffic.  The flat gradient buffer is full-size in both
   modes, so HBM use is the same.  Micro-steps without a collective leave every dW product queued
-  for one batched flush, as at world size 1.
+  for one batched flush, as at world size 1.  Precision differs: window mode sums the micro-steps
+  in the bf16 flat buffer (the GEMMs accumulate with beta = 1) before one bf16 reduce-scatter,
+  while micro mode adds each reduce-scattered chunk into an fp32 owner buffer.
+  tests/test_multirank_gpu.py bounds both against the world-1 run of the same global batch.
+* DDP ``grad_comm_dtype="fp32"``: each bucket is widened to fp32 right before its all-reduce (the
+  reference's torch DDP reduces fp32 gradients), AdamW reads the fp32 sum.
 """
 import os
 

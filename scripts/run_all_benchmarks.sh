@@ -1,33 +1,86 @@
 #!/usr/bin/env bash
 # Full benchmark suite on one 8x MI355X node: every strategy at 1/2/4/8 GPUs (reference:
 # scripts/run_all_benchmarks.sh ran {ddp,fsdp,zero2,zero3} x WS{2,4} as K8s jobs).
-# Each config: launch (torchrun) -> collect -> failure bookkeeping; then parse -> plot -> report.
+#  1. xGMI collective sweep (scripts/bench_collectives.py) at every multi-GPU world size ->
+#     summary/xgmi_buckets.json (and profiles/xgmi_buckets.json on real GPUs), which
+#     comm/topology.py reads to size the gradient buckets of every following run.
+#  2. Each config: launch (torchrun) -> collect -> failure bookkeeping.  Rows (STRATS):
+#       ddp fsdp zero2 zero3      the reference's four strategies, reference semantics
+#       fsdp_root                 FSDP with the reference's effective layout: ONE root FlatParameter
+#                                 (configs/fsdp/fsdp_reference_root.yaml)
+#       ddp_uniform fsdp_uniform  DDP / FSDP with ZeRO semantics (grad-accum 4, clip 1.0, WarmupLR)
+#       zero1                     ZeRO-2 engine with one reduce-scatter per window (opt-in row)
+#  3. parse -> plot -> report.
 # Like the reference it always exits 0; failed configs are listed in results/summary/failures.json.
 #
 #   ./scripts/run_all_benchmarks.sh [results-dir]
 #   env: STEPS, SEQ, TIER, WS_LIST, STRATS, TIMEOUT, HARNESS_EXTRA (extra harness flags),
-#        FORCE_NPROC (process slots when no GPU is visible, e.g. the gloo/CPU rehearsal)
+#        FORCE_NPROC (process slots when no GPU is visible, e.g. the gloo/CPU rehearsal),
+#        COLLECTIVES=0 (skip step 1), COLL_MAX_MB (largest swept message, default 512)
 set -uo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 RESULTS="${1:-$ROOT/results}"
 STEPS="${STEPS:-100}"; SEQ="${SEQ:-2048}"; TIER="${TIER:-A}"; TIMEOUT="${TIMEOUT:-900}"
-STRATS="${STRATS:-ddp fsdp zero2 zero3}"
+STRATS="${STRATS:-ddp fsdp zero2 zero3 fsdp_root ddp_uniform fsdp_uniform}"
 NGPU="${FORCE_NPROC:-$(python3 -c "import torch; print(torch.cuda.device_count())" 2>/dev/null || echo 0)}"
 read -r -a HX <<< "${HARNESS_EXTRA:-}"
 WS_LIST="${WS_LIST:-1 2 4 8}"
 mkdir -p "$RESULTS/raw" "$RESULTS/summary"
 FAILED=(); DONE=0
+export HSA_ENABLE_IPC_MODE_LEGACY="${HSA_ENABLE_IPC_MODE_LEGACY:-0}"
 echo "=================================================================="
 echo "  MI355X Distributed Training Benchmark Suite ($NGPU GPUs visible)"
 echo "=================================================================="
+
+# ---- 1. collective sweep -> bucket sizing profile
+PROFILE="$RESULTS/summary/xgmi_buckets.json"
+if [[ "${COLLECTIVES:-1}" != "0" ]]; then
+  if [[ -n "${FORCE_NPROC:-}" ]]; then CARGS=(--backend gloo --device cpu --max-mb "${COLL_MAX_MB:-4}" --iters 3 --warmup 1)
+  else CARGS=(--max-mb "${COLL_MAX_MB:-512}"); fi
+  for ws in $WS_LIST; do
+    [[ "$ws" -lt 2 || "$ws" -gt "$NGPU" ]] && continue
+    echo "---- collectives ws=$ws"
+    timeout -k 30 "$TIMEOUT" python -m torch.distributed.run --nnodes 1 --nproc-per-node "$ws" --max-restarts 0 \
+      --master-addr 127.0.0.1 --master-port "$((29500 + RANDOM % 1000))" "$ROOT/scripts/bench_collectives.py" \
+      --ops reduce_scatter,all_gather,all_reduce "${CARGS[@]}" --json "$RESULTS/summary/collectives_ws$ws.json" \
+      > "$RESULTS/collectives_ws$ws.log" 2>&1 || { FAILED+=("collectives-ws$ws"); echo "     FAILED"; }
+  done
+  python3 - "$PROFILE" "$RESULTS/summary" "${FORCE_NPROC:-}" "$ROOT/profiles/xgmi_buckets.json" <<'PY'
+import glob, json, os, re, shutil, sys
+out, d, forced, repo_copy = sys.argv[1:5]
+worlds = {}
+for p in sorted(glob.glob(os.path.join(d, "collectives_ws*.json"))):
+    worlds[re.search(r"ws(\d+)", p).group(1)] = json.load(open(p))
+if worlds:
+    json.dump({"source": "scripts/bench_collectives.py via run_all_benchmarks.sh",
+               "backend": "gloo-cpu" if forced else "rccl", "worlds": worlds}, open(out, "w"), indent=1)
+    if not forced:                      # real GPUs: this node's measurement becomes the default
+        shutil.copyfile(out, repo_copy)
+PY
+  [[ -f "$PROFILE" ]] && export DLTB_XGMI_PROFILE="$PROFILE"
+fi
+
+# ---- 2. benchmark matrix
+variant() {   # row name -> "engine strategy|extra harness flags"
+  case "$1" in
+    ddp|fsdp|zero2|zero3) echo "$1|" ;;
+    fsdp_root) echo "fsdp|--fsdp-config $ROOT/configs/fsdp/fsdp_reference_root.yaml --strategy-label fsdp_root" ;;
+    ddp_uniform|fsdp_uniform) echo "${1%_uniform}|--accum-semantics uniform --strategy-label $1" ;;
+    zero1) echo "zero2|--grad-reduce window --strategy-label zero1" ;;
+    *) echo "" ;;
+  esac
+}
 for s in $STRATS; do
+  spec="$(variant "$s")"
+  if [[ -z "$spec" ]]; then echo "unknown row $s"; FAILED+=("$s"); continue; fi
+  eng="${spec%%|*}"; read -r -a VX <<< "${spec#*|}"
   for ws in $WS_LIST; do
     if [[ "$ws" -gt "$NGPU" ]]; then echo "skip $s ws=$ws (only $NGPU GPUs)"; continue; fi
     job="bench-master-${s}-ws${ws}-seq${SEQ}"
     echo "---- $job"
-    if timeout -k 30 "$TIMEOUT" "$ROOT/scripts/launch_local.sh" --strategy "$s" --world-size "$ws" --seq-len "$SEQ" \
-         --tier "$TIER" --steps "$STEPS" --per-device-batch 1 --grad-accum 4 --results-dir "$RESULTS/raw" -- "${HX[@]}" \
-         > "$RESULTS/$job.log" 2>&1 \
+    if timeout -k 30 "$TIMEOUT" "$ROOT/scripts/launch_local.sh" --strategy "$eng" --world-size "$ws" --seq-len "$SEQ" \
+         --tier "$TIER" --steps "$STEPS" --per-device-batch 1 --grad-accum 4 --results-dir "$RESULTS/raw" \
+         -- "${VX[@]}" "${HX[@]}" > "$RESULTS/$job.log" 2>&1 \
        && "$ROOT/scripts/collect_results.sh" "$RESULTS/$job.log" "$RESULTS" "$job" "$RESULTS/raw"; then
       DONE=$((DONE + 1)); echo "     ok"
     else

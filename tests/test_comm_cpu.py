@@ -104,3 +104,22 @@ GPU2   XGMI         XGMI         0
 """
     links = parse_topology(txt)
     assert links[(0, 1)] == "XGMI" and (0, 0) not in links and len(links) == 6
+
+
+def test_alpha_beta_fit_and_measured_bucket(tmp_path, monkeypatch):
+    import json
+    from dltb.comm.collectives import ring_factor
+    from dltb.comm.topology import fit_alpha_beta, measured_params, recommend_bucket_mb
+    alpha, bus, world = 40.0, 250.0, 8
+    rows = [{"op": "reduce_scatter", "bytes": b, "time_us": alpha + b * ring_factor("reduce_scatter", world) / (bus * 1e3)}
+            for b in (1 << 20, 4 << 20, 16 << 20, 64 << 20)]
+    a, g = fit_alpha_beta(rows, "reduce_scatter", world)
+    assert abs(a - alpha) < 1e-6 and abs(g - bus) < 1e-6
+    p = tmp_path / "prof.json"
+    p.write_text(json.dumps({"worlds": {"8": rows}}))
+    monkeypatch.setenv("DLTB_XGMI_PROFILE", str(p))
+    assert measured_params(8)[2] == "measured" and measured_params(4)[2] == "default"
+    # alpha 40 us at 250 GB/s: need 40/0.2 us * 250 GB/s / (7/8) = 57 MB -> 64 MiB
+    assert recommend_bucket_mb(8) == 64.0
+    monkeypatch.setenv("DLTB_XGMI_PROFILE", str(tmp_path / "missing.json"))
+    assert measured_params(8)[2] == "default"

@@ -36,3 +36,24 @@ def test_suite_records_failures_and_still_exits_zero(tmp_path):
     _suite(tmp_path, "--fail-at-step 3", strats="ddp")
     failed = json.load(open(tmp_path / "summary" / "failures.json"))["failed"]
     assert failed == ["bench-master-ddp-ws1-seq64", "bench-master-ddp-ws2-seq64"]
+
+
+def test_suite_variant_rows_and_measured_bucket_profile(tmp_path, monkeypatch):
+    """fsdp_root (the reference's single root FlatParameter) and ddp_uniform rows land in the CSV
+    under their own names; the collective sweep writes the bucket profile that sizes the runs."""
+    _suite(tmp_path, "", strats="fsdp_root ddp_uniform")
+    df = pd.read_csv(tmp_path / "summary" / "metrics.csv")
+    assert sorted(zip(df.strategy, df.world_size)) == [("ddp_uniform", 1), ("ddp_uniform", 2),
+                                                       ("fsdp_root", 1), ("fsdp_root", 2)]
+    prof = json.load(open(tmp_path / "summary" / "xgmi_buckets.json"))
+    assert prof["backend"] == "gloo-cpu" and set(prof["worlds"]) == {"2"}
+    ops = {r["op"] for r in prof["worlds"]["2"]}
+    assert {"reduce_scatter", "all_gather", "all_reduce"} <= ops
+    from dltb.comm.topology import measured_params, recommend_bucket_mb
+    monkeypatch.setenv("DLTB_XGMI_PROFILE", str(tmp_path / "summary" / "xgmi_buckets.json"))
+    assert measured_params(2)[2] == "measured"
+    ext = json.load(open(tmp_path / "bench-master-fsdp_root-ws2-seq64_results" / "result.extended.json"))
+    assert ext["bucket_mb"] == recommend_bucket_mb(2)
+    assert ext["engine_config"]["wrap"] == "root" and ext["strategy_engine"] == "fsdp"
+    ext = json.load(open(tmp_path / "bench-master-ddp_uniform-ws2-seq64_results" / "result.extended.json"))
+    assert ext["engine_config"]["grad_accum"] == 4 and ext["accum_semantics"] == "uniform"
