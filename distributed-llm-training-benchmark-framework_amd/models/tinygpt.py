@@ -22,14 +22,12 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
-import os
 from types import SimpleNamespace
 
 import torch
 import torch.nn as nn
 
 from ..ops import functional as F_
-from ..ops.streams import GradStreams
 from ..parallel.runtime import EAGER, Unit
 from .config import ModelConfig
 
@@ -66,15 +64,10 @@ class TinyGPTBlock(nn.Module):
 
 
 # ============================================================================ fused Functions
-# DLTB_MASK_STREAM=1: generate the attention dropout mask on a side stream, concurrent with LN1 + QKV
-_MASK_STREAM = __import__("os").environ.get("DLTB_MASK_STREAM", "0") == "1"
-# DLTB_FUSE_MLP_DROPOUT=0: x2 = x1 + Dropout(m) as its own kernel instead of inside the next LayerNorm
-_FUSE_MLP_DROPOUT = os.environ.get("DLTB_FUSE_MLP_DROPOUT", "1") == "1"
-# DLTB_FUSE_DROPOUT_BWD=1: the consumer's LayerNorm backward kernel forms the producing block's MLP
-# Dropout backward + fc2 bias partials (one colpart launch less per layer).  Measured neutral on
-# MI355X (7.63 vs 7.62 ms, profiles/ab_fused_dropout_bwd_1gpu.jsonl: the hash work the 8-wave norm
-# kernel takes on costs what the launch saved), so the producing block's colpart stays the default.
-_FUSE_DROPOUT_BWD = os.environ.get("DLTB_FUSE_DROPOUT_BWD", "0") == "1"
+# Measured and removed (round 2 toggle pruning; records under profiles/ab_*.jsonl): dropout mask /
+# weight gradients / dQ on side streams (slower: two under-filling kernels slow each other down),
+# a standalone residual+dropout kernel (the fused LayerNorm form is faster), and the consumer's
+# LayerNorm backward forming the producer's MLP Dropout backward (neutral).
 
 
 class _EmbedFn(torch.autograd.Function):
@@ -120,9 +113,8 @@ class _BlockFn(torch.autograd.Function):
         cfg = model.cfg
         H, d = cfg.n_head, cfg.n_embd
         p = model.drop_p
-        par = GradStreams(x_in.device, enabled=_MASK_STREAM or None)
         lb = model.layer_buffer(i)          # layer-strided GEMM operands (batched weight gradients)
-        amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x_in, par)   # overlaps LN1 + QKV GEMM
+        amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x_in)
         if m_in is None:                    # block 0: the embedding output
             x = x_in
             _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False, y_out=lb and lb.h1)
@@ -132,7 +124,7 @@ class _BlockFn(torch.autograd.Function):
         qkv = F_.linear_fwd(h1, win, bin_)
         o, lse, amask = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
                                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i),
-                                    amask, par, o_out=lb and lb.o)
+                                    amask, o_out=lb and lb.o)
         a = F_.linear_fwd(o, wo, bo)
         x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
         f = F_.linear_fwd(h2, w1, b1)
@@ -142,15 +134,12 @@ class _BlockFn(torch.autograd.Function):
         ctx.model, ctx.i, ctx.lb = model, i, lb
         ctx.fused_prev = m_in is not None   # LN1 applied the previous block's MLP dropout
         ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g)
-        if not _FUSE_MLP_DROPOUT:           # standalone residual + dropout kernel
-            return F_.dropout(x1, m, p, rt.seed, model.site_mlp(i)), None
         return x1, m
 
     @staticmethod
-    def backward(ctx, dx2, dm_in):
-        # dx2 = d(x1 + Dropout(m)) from the consumer.  m's gradient (Dropout backward, with the fc2
-        # bias column sum) either comes from the consumer's LayerNorm backward (dm_in, engines with
-        # grad_write_ahead) or is formed here
+    def backward(ctx, dx2, dm_unused):
+        # dx2 = d(x1 + Dropout(m)) from the consumer; m's gradient (Dropout backward, with the fc2
+        # bias column sum) is formed here
         model, i = ctx.model, ctx.i
         rt, unit = model.rt, model.unit_blocks[i]
         (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g) = ctx.saved
@@ -163,30 +152,23 @@ class _BlockFn(torch.autograd.Function):
         dx2 = dx2.contiguous()
         s = [rt.grad_slot(unit, j) for j in range(12)]
         lb = ctx.lb
-        par = GradStreams(dx2.device)      # parameter-gradient work -> side stream (DLTB_SIDE_STREAM)
 
         def wgrad(j, dy, xin):             # dW_j (+)= dy^T xin: now, or queued and batched by the engine
-            if par.enabled and par.wgrad:
-                F_.linear_wgrad(dy, xin, s[j][0], None, s[j][1], par)
-            else:
-                rt.wgrad(unit, j, dy, xin, s[j][0], s[j][1])
+            rt.wgrad(unit, j, dy, xin, s[j][0], s[j][1])
 
         # the 8 bias / LayerNorm column sums: fused partials, reduced by ONE launch per block (or,
         # with the engine's shared reducer at world size 1, one launch for all blocks)
         shared = rt.grad_reducer()
         red = shared if shared is not None else F_.GradReducer()
         # MLP
-        if dm_in is not None:
-            dm = dm_in
-        else:
-            dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
-                                     out=lb and lb.dm)
+        dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
+                                 out=lb and lb.dm)
         wgrad(10, dm, g)
         dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
         df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
         wgrad(8, df, h2)
         dh2 = F_.linear_dgrad(df, w1, rt.weight_t(unit, 8, w1))
-        dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False, par,
+        dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False,
                           red, bias=("dx", s[5][0], s[5][1]), dx_out=lb and lb.dx1)
         # attention
         wgrad(4, dx1, o)
@@ -194,27 +176,16 @@ class _BlockFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv) if lb is None else lb.dqkv
         F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, amask,
                     dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
-                    1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i), par)
-        par.join()                                            # dQ (side) completes dqkv
+                    1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
         wgrad(2, dqkv, h1)
         dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
-        drop_prev = None
-        if ctx.fused_prev and rt.grad_write_ahead and _FUSE_DROPOUT_BWD:
-            # the previous block's Dropout(m') backward + fc2 bias sum, produced with dx in one kernel
-            ps = rt.grad_slot(model.unit_blocks[i - 1], 11)
-            plb = model.layer_buffer(i - 1) if lb is not None else None
-            drop_prev = (p, rt.seed, model.site_mlp(i - 1), plb and plb.dm, ps[0], ps[1])
-        dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False, par,
-                         red, bias=(dqkv, s[3][0], s[3][1]), drop=drop_prev)
-        dm_prev = None
-        if drop_prev is not None:
-            dx, dm_prev = dx
+        dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False,
+                         red, bias=(dqkv, s[3][0], s[3][1]))
         if shared is None:
             red.flush()
-        par.join()                                            # all of this unit's gradients written
         rt.grads_ready(unit)
         rt.release_backward(unit)
-        return dx, dm_prev, None, None
+        return dx, None, None, None
 
 
 class _HeadFn(torch.autograd.Function):
@@ -257,15 +228,13 @@ class _HeadFn(torch.autograd.Function):
         ctx.saved = None
         lnw, lnb = rt.acquire_backward(model.unit_head)
         wte = rt.acquire_tied(model.unit_embed)[0]
-        par = GradStreams(x.device)
         dw, acc_w = rt.grad_slot(model.unit_embed, 0)            # tied lm_head / wte
         hs, g = F_.scale_by(h, dloss, count)                      # g = dloss / count (device)
-        F_.linear_wgrad(dl, hs, dw, None, acc_w, par)              # side stream, overlaps dh
+        F_.linear_wgrad(dl, hs, dw, None, acc_w)
         dh = F_.head_dgrad(dl, wte, rt.weight_t(model.unit_embed, 0, wte), g)
         gw, acc = rt.grad_slot(model.unit_head, 0)
         gb, _ = rt.grad_slot(model.unit_head, 1)
-        dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False, par)
-        par.join()
+        dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False)
         rt.grads_ready(model.unit_head)
         rt.release_backward(model.unit_head)
         return dx, None, None, None, None

@@ -4,8 +4,6 @@
 GEMMs are plain ``torch`` matmuls (hipBLASLt on ROCm); gradient-producing GEMMs write straight
 into the engine's flat gradient slots (``out=`` / ``addmm_``) so no gradient is ever copied.
 """
-import os
-
 import torch
 
 from . import ref
@@ -41,10 +39,6 @@ def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0, y_out=None):
 
 # colpart segment kinds (csrc/colreduce.hip)
 _PLAIN, _GELU, _DROP, _LN, _RMS = 0, 1, 2, 3, 4
-
-# DLTB_FUSED_NORM_BWD=0 restores the two-launch norm backward (dx kernel + colpart partials)
-_FUSED_NORM_BWD = os.environ.get("DLTB_FUSED_NORM_BWD", "1") == "1"
-
 
 class GradReducer:
     """Batches the column reductions of one backward unit: producer kernels write fp32 column
@@ -88,9 +82,9 @@ class GradReducer:
             self.parts, self.outs, self.acc = [], [], []
 
 
-def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=None, bias=None,
+def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, red=None, bias=None,
              dx_out=None, drop=None):
-    """dx on the current stream; dgamma/dbeta (parameter gradients) on ``par``'s side stream.
+    """dx, and dgamma/dbeta written into their gradient slots.
 
     With a :class:`GradReducer` the dgamma/dbeta partials (and, with ``bias=(src, slot, acc)``, the
     column sum of ``src`` -- ``src="dx"`` meaning this call's output) come from ONE colpart launch
@@ -101,7 +95,7 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
     the GPU (the previous block's MLP dropout and fc2 bias gradient)."""
     if drop is not None:
         dp, dseed, dsite, dm_out, db, db_acc = drop
-        if red is not None and _gpu(dy) and _FUSED_NORM_BWD and ext().norm_bwd_fused_supported(dy.shape[-1]):
+        if red is not None and _gpu(dy) and ext().norm_bwd_fused_supported(dy.shape[-1]):
             C = ext()
             dm = torch.empty_like(dy) if dm_out is None else dm_out
             dx, part = C.norm_bwd_fused(dy, s, w, mean, rstd, dres, rms, False, dx_out, dm, dp,
@@ -118,14 +112,14 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
                     parts = C.colpart([_PLAIN], [bias[0]], [None], [None], [None], [None], 0.0, None, [0])
                     red.add(parts[0][0], bias[1], bias[2])
             return dx, dm
-        dx = norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par, red, bias, dx_out)
+        dx = norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, red, bias, dx_out)
         red_local = red if red is not None else GradReducer()
         dm = dropout_bwd_bias(dx, dp, dseed, dsite, db, db_acc, red_local, out=dm_out)
         if red is None:
             red_local.flush()
         return dx, dm
     if red is not None:
-        if _gpu(dy) and _FUSED_NORM_BWD and ext().norm_bwd_fused_supported(dy.shape[-1]):
+        if _gpu(dy) and ext().norm_bwd_fused_supported(dy.shape[-1]):
             # one kernel: dx + gamma / beta partials (+ the column partials of dx itself)
             C = ext()
             has_bias = bias is not None and bias[1] is not None
@@ -161,13 +155,7 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, par=None, red=
             ref.colsum_into(dx if isinstance(bias[0], str) else bias[0], bias[1], bias[2])
         return dx
     if _gpu(dy):
-        C = ext()
-        if par is None or not par.enabled:
-            return C.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
-        dx = C.norm_bwd_dx(dy, s, w, mean, rstd, dres, rms)
-        with par.fork(dy, s, mean, rstd):
-            C.norm_bwd_dgamma(dy, s, mean, rstd, gw, gb, accumulate, rms)
-        return dx
+        return ext().norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
     return ref.norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms)
 
 
@@ -294,46 +282,33 @@ def head_dgrad(dl, w, wt, g):
 
 
 # ------------------------------------------------------------------------------ attention
-def attn_mask(B, T, Hq, p, seed, site, like, par=None):
-    """Packed dropout keep-bits for attention (GPU only; launched on the side stream so it overlaps
-    the QKV projection).  Returns None on the CPU or without dropout."""
+def attn_mask(B, T, Hq, p, seed, site, like):
+    """Packed dropout keep-bits for attention (GPU only).  Returns None on the CPU or without
+    dropout."""
     if p <= 0 or not like.is_cuda:
         return None
-    if par is not None and par.enabled:
-        with par.fork():
-            m = ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, like)
-        m.record_stream(par.main)
-        return m
     return ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, like)
 
 
-def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site, mask=None, par=None, o_out=None):
+def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site, mask=None, o_out=None):
     """Returns (o, lse, aux); ``aux`` (the packed dropout mask on the GPU) goes back into attn_bwd."""
     if _gpu(q):
         if p > 0 and mask is None:
             mask = ext().attn_mask(B, T, Hq, p, seed.device_tensor, site, q)
-        if par is not None:
-            par.join()                      # the mask was produced on the side stream
         o, lse = ext().attn_fwd(q, k, v, mask if p > 0 else None, B, T, Hq, Hkv, scale, causal, p, o_out)
         return o, lse, (mask if p > 0 else None)
     o, lse = ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site)
     return _into(o_out, o), lse, None
 
 
-def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site, par=None):
-    """dK/dV (key-major kernel) on the current stream, dQ (query-major kernel) concurrently on
-    ``par``'s side stream.  Call ``par.join()`` before reading dq."""
+def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site):
+    """dQ (query-major kernel, which also forms delta = rowsum(dO * O) for its rows), then dK/dV
+    (key-major kernel, reading that delta)."""
     if _gpu(q):
         C = ext()
         m = aux if p > 0 else None
-        if par is not None and par.enabled and par.attn:
-            delta = C.attn_bwd_delta(o, do, B, T, Hq)
-            with par.fork(q, k, v, do, lse, delta, m):
-                C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p)
-        else:
-            # the dQ pass computes delta = rowsum(dO * O) for its rows and stores it for dK/dV
-            delta = torch.empty_like(lse)
-            C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p, o)
+        delta = torch.empty_like(lse)
+        C.attn_bwd_part(1, q, k, v, do, lse, delta, m, dq, None, B, T, Hq, Hkv, scale, causal, p, o)
         C.attn_bwd_part(0, q, k, v, do, lse, delta, m, dk, dv, B, T, Hq, Hkv, scale, causal, p)
     else:
         ref.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, T, Hq, Hkv, scale, causal, p, seed, site)
@@ -353,13 +328,8 @@ def linear_dgrad(dy2d, w, wt=None):
     return torch.mm(dy2d, w)
 
 
-def linear_wgrad(dy2d, x2d, dw, db, accumulate, par=None):
-    """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy).  With ``par`` the
-    work runs on the side stream (parameter gradients are off the critical path)."""
-    if par is not None and par.enabled and par.wgrad:
-        with par.fork(dy2d, x2d):
-            linear_wgrad(dy2d, x2d, dw, db, accumulate)
-        return
+def linear_wgrad(dy2d, x2d, dw, db, accumulate):
+    """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy)."""
     if dw is not None:
         if accumulate:
             dw.addmm_(dy2d.t(), x2d)

@@ -99,21 +99,7 @@ class ReplicatedEngine(Engine):
         self._ag_pending = {}    # bucket -> async all-gather of updated parameters (deferred step)
         self._defer_opt = (self.stage >= 1 and self.world > 1 and
                            bool(cfg.extra.get("defer_opt", os.environ.get("DLTB_DEFER_OPT", "1") == "1")))
-        # world 1, ZeRO-1/2 (one AdamW segment per bucket), opt-in: the deferred update runs on a
-        # side stream, one launch per bucket in forward order, and each unit's forward waits only
-        # for its own bucket's event.  Bitwise the in-order step (tests/test_graphs_gpu.py), but
-        # measured neutral on MI355X (TinyGPT-A: 7.694 vs 7.702 ms graphed, 7.651 vs 7.645 eager,
-        # profiles/ab_overlap_opt_1gpu.jsonl): AdamW's ~60k workgroups take the CUs and the HBM
-        # bandwidth the forward would have used, so the forward slows by what the overlap hides.
-        self._overlap_opt = (self.stage >= 1 and self.world == 1 and dev.type == "cuda" and
-                             len(opt_segs) == len(L.buckets) and
-                             bool(cfg.extra.get("overlap_opt", os.environ.get("DLTB_OVERLAP_OPT", "0") == "1")))
-        self._opt_ev = {}        # bucket -> event recorded after its AdamW launch (overlapped step)
-        self._opt_inflight = False
-        if self._overlap_opt:
-            self._defer_opt = True
-            self._opt_stream = torch.cuda.Stream(device=dev)
-        self._cache_wt = bool(cfg.extra.get("cache_weight_t", os.environ.get("DLTB_CACHE_WT", "1") == "1"))
+        self._cache_wt = True    # cached W^T of every matrix for the NT-form dgrad GEMMs
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
         # weight gradients queued and issued as strided-batched GEMMs (parallel/wgrad.py): world 1
@@ -124,8 +110,7 @@ class ReplicatedEngine(Engine):
         # column sums of ALL blocks are reduced by one or two colreduce_multi launches at its end
         # instead of one launch per block, and the QKV-bias partials of block i ride along with
         # block i-1's dropout colpart launch instead of a launch of their own
-        self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda" and bool(
-            cfg.extra.get("shared_colreduce", os.environ.get("DLTB_SHARED_COLREDUCE", "1") == "1"))) else None
+        self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda") else None
         self._launched = [False] * len(L.buckets)
         nbytes = L.total * (4 if self.comm_f32 is not None else elem)
         if self.world > 1:
@@ -182,10 +167,6 @@ class ReplicatedEngine(Engine):
                     C.transpose_into(w, wt)
 
     def acquire(self, unit):
-        if self._opt_ev:
-            ev = self._opt_ev.pop(self._bucket_of.get(id(unit)), None)
-            if ev is not None:
-                torch.cuda.current_stream().wait_event(ev)
         if self._ag_pending:
             b = self._bucket_of.get(id(unit))
             w = self._ag_pending.pop(b, None)
@@ -252,7 +233,6 @@ class ReplicatedEngine(Engine):
             self._written.clear()         # the full gradient buffer is reduced every micro-step
 
     def _finish_backward(self):
-        self._join_opt_stream()
         if self._red is not None:
             self._red.flush()
         self._wq.flush()                                        # world 1: every block in one batch
@@ -289,20 +269,6 @@ class ReplicatedEngine(Engine):
         self.opt.step(g, lr, gscale)
 
     def _deferred_optimizer_step(self, lr):
-        if self._overlap_opt:
-            main, side = torch.cuda.current_stream(), self._opt_stream
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                g = self._owner_grad()
-                gscale = self._clip_coef([g], 1.0 / self.accum, sharded=True)
-                self.opt.prepare(lr)
-                for b in reversed(range(len(self.layout.buckets))):  # forward order
-                    self.opt.launch_segment(b, g, gscale)
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    self._opt_ev[b] = ev
-            self._opt_inflight = True
-            return
         self._update(lr)
         for b in reversed(range(len(self.layout.buckets))):     # forward order: embedding first
             bk = self.layout.buckets[b]
@@ -310,16 +276,7 @@ class ReplicatedEngine(Engine):
             mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
             self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
 
-    def _join_opt_stream(self):
-        """Make the compute stream wait for the overlapped optimizer step (a no-op once every
-        bucket has been acquired, but the side stream must rejoin before a graph capture ends)."""
-        if self._opt_inflight:
-            torch.cuda.current_stream().wait_stream(self._opt_stream)
-            self._opt_ev.clear()
-            self._opt_inflight = False
-
     def _wait_param_gathers(self):
-        self._join_opt_stream()
         for w in self._ag_pending.values():
             w.wait()
         self._ag_pending.clear()

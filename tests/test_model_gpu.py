@@ -66,26 +66,3 @@ def test_engine_step_every_strategy(strategy):
     assert losses[-1] < losses[0], losses      # memorising one batch must reduce the loss
     sd = eng.full_state_dict()
     assert sd["transformer.wte.weight"].shape == (cfg.vocab_size, cfg.n_embd)
-
-
-def test_side_stream_overlap_is_bitwise_identical(monkeypatch):
-    """Scheduling parameter-gradient work on the side stream must not change any result."""
-    torch.manual_seed(0)
-    cfg = _cfg(T=256, layers=2, dropout=0.1)
-    base = build_model(cfg).to("cuda", torch.bfloat16)
-    grads = []
-    for flag in ("0", "1"):  # off (default) vs on
-        monkeypatch.setenv("DLTB_SIDE_STREAM", flag)
-        m = copy.deepcopy(base)
-        m.rt = ParamRuntime()
-        sd = StepSeed(3, device="cuda")
-        sd.next()
-        m.rt.seed = sd
-        m.train()
-        idx = torch.randint(0, cfg.vocab_size, (1, 256), generator=torch.Generator().manual_seed(1)).cuda()
-        _, loss = m(idx, idx)
-        loss.backward()
-        torch.cuda.synchronize()
-        grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
-    for n in grads[0]:
-        assert torch.equal(grads[0][n], grads[1][n]), n

@@ -18,3 +18,9 @@ def test_world2_host_staged_equals_world1_gpu(tmp_path):
     assert set(ws1) == set(ws2)
     bad = compare(ws1, ws2, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
     assert not bad, bad
+    # DLTB_DEFER_OPT=0: the ZeRO-1/2 update + all-gather at the boundary instead of deferred into
+    # the next micro-step's forward (per-bucket waits in acquire)
+    ws2n = run(tmp_path / "ws2n.pt", 2, "cuda", extra=("--cases", "zero2,zero2_window"),
+               env_extra={"DLTB_COMM": "host", "DLTB_DEFER_OPT": "0"}, timeout=600)
+    bad = compare({k: ws1[k] for k in ws2n}, ws2n, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
+    assert not bad, bad
