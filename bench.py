@@ -62,7 +62,9 @@ def build_parser():
     ap.add_argument("--grad-reduce", default="micro", choices=["micro", "window"],
                     help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed stage 2, default) or "
                          "once per accumulation window (ZeRO-1 communication, reported as zero1-dpN)")
-    ap.add_argument("--grad-comm-dtype", default="bf16", choices=["bf16", "fp32"],
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
+                    help="compute dtype (fp16: dynamic loss scaling, the reference's DDP/FSDP precision)")
+    ap.add_argument("--grad-comm-dtype", default="compute", choices=["compute", "fp32"],
                     help="DDP gradient all-reduce dtype (fp32 = the reference's torch DDP)")
     ap.add_argument("--fsdp-wrap", default="block", choices=["block", "root"],
                     help="FSDP unit layout: per transformer block, or the reference's single root FlatParameter")
@@ -135,9 +137,10 @@ def run_rank(args) -> int:
             model = build_model(mcfg)
         bucket_mb = args.bucket_mb if args.bucket_mb is not None else recommend_bucket_mb(world)
         h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None,
-                               grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype="bf16",
+                               grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype=args.dtype,
                                bucket_mb=bucket_mb, seed=42, grad_reduce=args.grad_reduce,
-                               grad_comm_dtype=args.grad_comm_dtype, fsdp_wrap=args.fsdp_wrap)
+                               grad_comm_dtype=args.grad_comm_dtype,
+                               fsdp_wrap=args.fsdp_wrap)
         engine, ecfg = _engine_for(h, model, device)
         ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
         batches = make_batcher("device", ds, args.per_device_batch, world, rank, args.strategy, device)
@@ -215,7 +218,7 @@ def run_rank(args) -> int:
                 "higher_is_better": True,
                 "scaling": "weak",
                 "vs_baseline": value / BASELINE_TPS if (args.tier == "A" and args.seq_len == 2048) else None,
-                "dtype": "bf16" if cuda else "fp32",
+                "dtype": args.dtype if cuda else "fp32",
                 "data": "synthetic tokens (fixed random table, seed 42), random-init weights",
                 "config": {"model": _model_name(args.tier, mcfg),
                            "global_batch": args.per_device_batch * accum * world,

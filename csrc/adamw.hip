@@ -42,6 +42,7 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
     const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, const float* __restrict__ hp,
     float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
   if (hp) {   // step-dependent hyper-parameters from device memory (HIP-graph replays)
+    if (hp[3] != 0.f) return;   // dynamic loss scaling found an inf / nan: the step is skipped
     lr = hp[0];
     step_size = hp[1];
     inv_sqrt_bc2 = hp[2];
@@ -121,6 +122,49 @@ __global__ void clip_coef_kernel(const float* __restrict__ norm_sq, float max_no
   if (norm_out) norm_out[0] = nrm;
 }
 
+// Dynamic loss scaling with torch.amp.GradScaler's semantics (train_harness.py:334-335, 371-376),
+// decided on the device so no step ever waits on the host:
+//   state = [scale S, growth tracker, optimizer steps taken, steps skipped]
+//   norm_sq = sum of squares of the S-scaled gradients (all-reduced where sharded); an inf or nan
+//   gradient makes it non-finite (fp16 gradients cannot overflow the fp32 sum: 65504^2 * 2^28).
+// found inf -> hp[3] = 1 (the AdamW kernel returns at once: master, moments and step count stay),
+//              S *= backoff, tracker = 0;
+// otherwise -> coef = extra * clip(unscaled norm) / S, hp[1..2] = bias corrections of the device
+//              step count, tracker += 1, S *= growth when it reaches growth_interval.
+// hp[0] (lr) is the host's upload (FlatAdamW.prepare) and is left alone.
+__global__ void amp_step_kernel(const float* __restrict__ norm_sq, float* __restrict__ state,
+                                float* __restrict__ coef, float* __restrict__ norm_out,
+                                float* __restrict__ hp, float max_norm, float extra_scale, float beta1,
+                                float beta2, float growth, float backoff, float growth_interval) {
+  const float S = state[0];
+  const float nsq = norm_sq[0];
+  if (!isfinite(nsq)) {
+    state[0] = S * backoff;
+    state[1] = 0.f;
+    state[3] += 1.f;
+    hp[3] = 1.f;
+    coef[0] = 0.f;
+    if (norm_out) norm_out[0] = nsq;
+    return;
+  }
+  const float inv = 1.f / S;
+  const float nrm = sqrtf(nsq) * inv * extra_scale;
+  const float c = max_norm > 0.f ? fminf(1.f, max_norm / (nrm + 1e-6f)) : 1.f;
+  coef[0] = c * extra_scale * inv;
+  if (norm_out) norm_out[0] = nrm;
+  const float t = state[2] + 1.f;
+  state[2] = t;
+  hp[1] = hp[0] / (1.f - powf(beta1, t));
+  hp[2] = 1.f / sqrtf(1.f - powf(beta2, t));
+  hp[3] = 0.f;
+  float tr = state[1] + 1.f;
+  if (tr >= growth_interval) {
+    state[0] = S * growth;
+    tr = 0.f;
+  }
+  state[1] = tr;
+}
+
 __global__ __launch_bounds__(256) void fill_f32_kernel(float* __restrict__ x, long n, float v) {
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
     x[i] = v;
@@ -164,6 +208,13 @@ void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* no
                     float extra_scale, hipStream_t st) {
   hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, st, norm_sq, max_norm, coef, norm_out,
                      extra_scale);
+}
+
+void dltb_amp_step(const float* norm_sq, float* state, float* coef, float* norm_out, float* hp,
+                   float max_norm, float extra_scale, float beta1, float beta2, float growth,
+                   float backoff, int growth_interval, hipStream_t st) {
+  hipLaunchKernelGGL(amp_step_kernel, dim3(1), dim3(1), 0, st, norm_sq, state, coef, norm_out, hp,
+                     max_norm, extra_scale, beta1, beta2, growth, backoff, (float)growth_interval);
 }
 
 void dltb_fill_f32(float* x, long n, float v, hipStream_t st) {

@@ -66,7 +66,7 @@ struct AttnArgs {
 DLTB_DEV bfx8 acc_to_frag(const f32x16& x, int s) {
   bfx8 f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = (__bf16)x[8 * s + j];
+  for (int j = 0; j < 8; ++j) f[j] = (h16_t)x[8 * s + j];
   return f;
 }
 
@@ -172,7 +172,7 @@ DLTB_DEV void static_for(F&& f) {
 
 template <int D>
 DLTB_DEV bfx8 pack_frag(const f32x16& x, int s) {      // regs 8s .. 8s+7 -> bf16 B operand
-  typedef __bf16 bfx2 __attribute__((ext_vector_type(2)));
+  typedef h16_t bfx2 __attribute__((ext_vector_type(2)));
   typedef float f32x2 __attribute__((ext_vector_type(2)));
   bfx8 f;
 #pragma unroll

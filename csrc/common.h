@@ -27,23 +27,40 @@
   } while (0)
 #endif
 
-typedef uint16_t bf16_t;                                     // raw bf16 bits
+// 16-bit storage format of this translation unit.  Every kernel file is compiled twice
+// (csrc/build.py): DLTB_F16=0 -> bf16 (the default compute dtype), DLTB_F16=1 -> IEEE fp16 (the
+// reference's DDP/FSDP autocast precision; host entry points renamed dltb_*_f16).  Tensors are
+// moved as raw 16-bit words (bf16_t) and converted to fp32 at the arithmetic by the helpers below,
+// so the kernel bodies are format-independent; the MFMA operand type follows h16_t.
+#ifndef DLTB_F16
+#define DLTB_F16 0
+#endif
+typedef uint16_t bf16_t;                                     // raw 16-bit float bits (bf16 or fp16)
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));    // MFMA A/B fragment (4 VGPRs)
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 
+#if DLTB_F16
+typedef _Float16 h16_t;
+DLTB_DEV float bf2f(bf16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+DLTB_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (_Float16)f); }
+DLTB_DEV float lo_bf(uint32_t w) { return bf2f((bf16_t)(w & 0xFFFFu)); }
+DLTB_DEV float hi_bf(uint32_t w) { return bf2f((bf16_t)(w >> 16)); }
+#else
+typedef __bf16 h16_t;
 DLTB_DEV float bf2f(bf16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
 DLTB_DEV bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
-// two floats -> packed bf16x2 in one dword (low = a)
+DLTB_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+DLTB_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+#endif
+// two floats -> packed 16-bit x2 in one dword (low = a)
 DLTB_DEV uint32_t pack_bf2(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
-DLTB_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
-DLTB_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
 
 // unpack 8 bf16 held in a uint4 into floats
 DLTB_DEV void unpack8(const uint4& v, float* f) {

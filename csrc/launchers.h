@@ -77,6 +77,10 @@ void dltb_sumsq(const void* x, bool bf16, long n, float* out, float* part, hipSt
 void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* norm_out,
                     float extra_scale, hipStream_t st);
 void dltb_fill_f32(float* x, long n, float v, hipStream_t st);
+// dynamic loss scaling step (adamw.hip): state f32[4] = [scale, tracker, steps taken, skipped]
+void dltb_amp_step(const float* norm_sq, float* state, float* coef, float* norm_out, float* hp,
+                   float max_norm, float extra_scale, float beta1, float beta2, float growth,
+                   float backoff, int growth_interval, hipStream_t st);
 
 // attention.hip
 bool dltb_attn_supported(int D, int T);
@@ -100,6 +104,8 @@ int dltb_attn_dkdv_gsplit(int B, int T, int Hq, int Hkv, int causal);
 void dltb_attn_init_attributes();
 
 // ---- batched column reductions (colreduce.hip)
+#ifndef DLTB_LAUNCHER_TYPES   // types once (launchers_f16.h repeats only the declarations)
+#define DLTB_LAUNCHER_TYPES
 enum { DLTB_COLPART_PLAIN = 0, DLTB_COLPART_GELU = 1, DLTB_COLPART_DROP = 2, DLTB_COLPART_LN = 3,
        DLTB_COLPART_RMS = 4 };
 #define DLTB_COLRED_MAX 64   // segments per colreduce_multi launch (kernel-argument struct: 2 KiB)
@@ -118,6 +124,7 @@ struct DltbColRedSeg {
   uint16_t* out;
   int P, k, accumulate;
 };
+#endif
 int dltb_colpart_partials(int N);
 void dltb_colpart(const DltbColPartSeg* segs, int nseg, int P, uint32_t thr16, float drop_scale,
                   const int64_t* seed, hipStream_t st);

@@ -15,12 +15,16 @@
 
 namespace {
 
-typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+typedef h16_t bfx8 __attribute__((ext_vector_type(8)));      // 8 x (bf16 | fp16): one A/B fragment
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 DLTB_DEV f32x16 mfma32(bfx8 a, bfx8 b, f32x16 c) {
+#if DLTB_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
 }
 
 template <int D>

@@ -469,7 +469,7 @@ void dltb_norm_bwd_dgamma(const void* dy, const void* s, const float* mean, cons
 }
 
 // ---- fused backward (dx + column partials); rows per wave chosen for >= 256 workgroups
-int dltb_norm_bwd_fused_rpw(int N) {
+static int dltb_norm_bwd_fused_rpw(int N) {
   int rpw = N / (kFusedWaves * 256);
   return rpw < 1 ? 1 : rpw;
 }

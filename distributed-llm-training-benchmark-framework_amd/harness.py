@@ -38,7 +38,8 @@ from .utils.gemm_tuning import flush_tunableop, setup_tunableop
 from .utils.platform import MI355X_DENSE_BF16_FLOPS, device_info
 from .utils.timers import PhaseTimers
 
-DTYPES = {"bf16": torch.bfloat16, "fp32": torch.float32}
+# bf16: the ZeRO configs' precision; fp16: the reference's DDP/FSDP autocast + GradScaler path
+DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
 
 
 def build_parser():
@@ -69,9 +70,12 @@ def build_parser():
     p.add_argument("--grad-reduce", choices=["micro", "window"], default="micro",
                    help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed) or once per "
                         "accumulation window")
-    p.add_argument("--grad-comm-dtype", choices=["bf16", "fp32"], default="bf16",
-                   help="DDP gradient all-reduce dtype (fp32 = the reference's torch DDP)")
-    p.add_argument("--dtype", choices=list(DTYPES), default="bf16")
+    p.add_argument("--grad-comm-dtype", choices=["auto", "bf16", "fp16", "fp32"], default="auto",
+                   help="DDP gradient all-reduce dtype: the compute dtype or fp32; auto = fp32 when DDP "
+                        "runs the reference's fp16 path (torch DDP reduces fp32 grads), else the compute dtype")
+    p.add_argument("--dtype", choices=["auto"] + list(DTYPES), default="auto",
+                   help="compute dtype; auto = the reference's precision per strategy: fp16 + dynamic loss "
+                        "scaling for ddp / fsdp (autocast + GradScaler), bf16 for zero2 / zero3 (DS configs)")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda" if torch.cuda.is_available() else "cpu")
     p.add_argument("--bucket-mb", type=float, default=None,
                    help="gradient bucket cap (MiB); default: comm.topology.recommend_bucket_mb(world), "
@@ -119,7 +123,7 @@ def _engine_for(args, model, device):
     cfg = engine_config(args.strategy, args.grad_accum, args.accum_semantics, ds, fc,
                         compute_dtype=DTYPES[args.dtype], bucket_mb=args.bucket_mb, seed=args.seed,
                         grad_reduce=getattr(args, "grad_reduce", "micro"))
-    cfg.extra["grad_comm_dtype"] = getattr(args, "grad_comm_dtype", "bf16")
+    cfg.extra["grad_comm_dtype"] = "fp32" if getattr(args, "grad_comm_dtype", None) == "fp32" else "compute"
     return make_engine(model, cfg, device), cfg
 
 
@@ -130,6 +134,12 @@ def train(args):
         from .comm.topology import recommend_bucket_mb
         args.bucket_mb = recommend_bucket_mb(world)
     label = args.strategy_label or args.strategy
+    if args.dtype == "auto":
+        args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
+    if args.grad_comm_dtype == "auto":
+        args.grad_comm_dtype = "fp32" if (args.strategy == "ddp" and args.dtype == "fp16") else args.dtype
+    if args.grad_comm_dtype not in ("fp32", args.dtype):
+        raise ValueError(f"--grad-comm-dtype {args.grad_comm_dtype}: must be fp32 or the compute dtype {args.dtype}")
     device = setup_distributed(world, rank, local_rank, args.master_addr, args.master_port, args.device,
                                args.timeout_min, args.debug_collectives)
     is_main = rank == 0
@@ -294,6 +304,7 @@ def train(args):
             "grad_comm_dtype": args.grad_comm_dtype, "strategy_engine": args.strategy, "bucket_mb": args.bucket_mb, "data_loader": args.data_loader,
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
             "phase_times_ms": timers.summary() if timers is not None else None,
+            "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
         }
         if is_main:
             print_result(record)

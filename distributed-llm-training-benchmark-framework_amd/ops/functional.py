@@ -272,7 +272,7 @@ def head_dgrad(dl, w, wt, g):
     """dX = g * dL W for an LM head with weight W [V, d].  On MI355X with a cached W^T this is the
     split-K MFMA GEMM (NT form, g applied as a device alpha in the split-K reduction): K = V is
     long and the output (tokens x d) small, which hipBLASLt's NN kernels handle poorly."""
-    if _gpu(dl) and wt is not None and dl.stride(1) == 1:
+    if _gpu(dl) and wt is not None and dl.stride(1) == 1 and dl.dtype == torch.bfloat16:
         M, K = dl.shape
         N = wt.shape[0]
         C = ext()

@@ -32,6 +32,10 @@ class FlatAdamW:
         self._tables = None
         self._seg_blocks = []    # segment -> (first, end) rows of the block tables (contiguous)
         self.hp = None
+        # compute-dtype copies written by the kernel: bf16 or fp16 (all segments share one)
+        dts = {dst.dtype for _, _, dst in self.segments}
+        assert len(dts) <= 1, "AdamW segments must share one compute dtype"
+        self.dst_f16 = dts == {torch.float16}
         if master.is_cuda:
             self._build_tables()
             self.hp = torch.zeros(4, dtype=torch.float32, device=master.device)
@@ -78,7 +82,7 @@ class FlatAdamW:
     def launch(self, grad: torch.Tensor, gscale: torch.Tensor = None):
         b1, b2 = self.betas
         ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, *self._tables, gscale,
-                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp)
+                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16)
 
     def launch_segment(self, i: int, grad: torch.Tensor, gscale: torch.Tensor = None):
         """The update of segment ``i`` alone (one launch over a slice of the block tables; the
@@ -89,7 +93,7 @@ class FlatAdamW:
         b1, b2 = self.betas
         ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, self._tables[0][lo:hi],
                     self._tables[1][lo:hi], *self._tables[2:], gscale,
-                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp)
+                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16)
 
     @torch.no_grad()
     def step(self, grad: torch.Tensor, lr: float, gscale: torch.Tensor = None):

@@ -23,6 +23,7 @@ import torch
 from ..comm import Comm
 from ..ops._ext import ext
 from ..ops.rng import StepSeed
+from ..optim.amp import DynamicLossScaler
 from ..optim.sched import build_scheduler
 from .runtime import ParamRuntime, Unit
 
@@ -64,6 +65,9 @@ class Engine(ParamRuntime):
         self.world, self.rank = self.comm.world, self.comm.rank
         self.accum = max(1, int(cfg.grad_accum))
         self.compute_dtype = cfg.compute_dtype if self.device.type == "cuda" else torch.float32
+        # fp16 compute (the reference's DDP/FSDP autocast): dynamic loss scaling, decided on the device
+        self.scaler = DynamicLossScaler(self.device, **cfg.extra.get("loss_scale_args", {})) \
+            if cfg.extra.get("loss_scaling") else None
         self.seed = StepSeed(cfg.seed, self.rank, self.device)
         self.sched = build_scheduler(cfg.scheduler, cfg.lr)
         self.micro = 0
@@ -107,7 +111,7 @@ class Engine(ParamRuntime):
         return loss
 
     def backward(self, loss):
-        loss.backward()
+        loss.backward(self.scaler.grad_output if self.scaler is not None else None)
         self._finish_backward()
 
     def step(self):
@@ -217,9 +221,35 @@ class Engine(ParamRuntime):
         else:
             out += t.float().pow(2).sum()
 
+    def _apply_update(self, g, lr: float, extra_scale: float, sharded: bool):
+        """Clip coefficient (+ loss-scale unscale / skip decision) and the fused AdamW update of the
+        owner gradient ``g``.  With a loss scaler the AdamW hyper-parameters are uploaded first:
+        ``amp_step`` overwrites their bias corrections (device step count) and the skip flag."""
+        if self.scaler is None:
+            self.opt.step(g, lr, self._clip_coef([g], extra_scale, sharded))
+        elif g.is_cuda:
+            self.opt.prepare(lr)
+            self.opt.launch(g, self._clip_coef([g], extra_scale, sharded))
+        else:
+            gscale = self._clip_coef([g], extra_scale, sharded)
+            if not self.scaler.last_skipped:
+                self.opt.step(g, lr, gscale)
+
     def _clip_coef(self, grads, extra_scale: float, sharded: bool):
         """Device gradient scale = extra_scale * min(1, clip / ||extra_scale * g||).  Also records
-        the global gradient norm in ``self.grad_norm`` (device tensor)."""
+        the global gradient norm in ``self.grad_norm`` (device tensor).  With a loss scaler the norm
+        pass is also the inf check and the scale folds 1/S in (optim/amp.py)."""
+        if self.scaler is not None:
+            self._norm_sq.zero_()
+            for g in grads:
+                self._sumsq_into(g, self._norm_sq)
+            if sharded and self.world > 1:
+                self.comm.all_reduce(self._norm_sq, async_op=False)
+            if self.grad_norm is None:
+                self.grad_norm = torch.zeros(1, device=self.device)
+            self.scaler.step(self._norm_sq, self._gscale, self.grad_norm, self.opt.hp, float(self.cfg.grad_clip),
+                             extra_scale, self.opt.betas)
+            return self._gscale
         want_norm = self.cfg.grad_clip > 0 or self.cfg.extra.get("track_grad_norm", False)
         if not want_norm:
             self._gscale.fill_(extra_scale)
@@ -254,7 +284,8 @@ class Engine(ParamRuntime):
         return {"format": "dltb-engine-v1", "engine": type(self).__name__, "strategy": self.cfg.strategy,
                 "world": self.world, "rank": self.rank, "accum": self.accum, "micro": self.micro,
                 "opt_steps": self.opt_steps, "seed_state": str(self.seed.state),
-                "optimizer": self.opt.state_dict()}
+                "optimizer": self.opt.state_dict(),
+                "loss_scaler": self.scaler.state_dict() if self.scaler is not None else None}
 
     def load_state_dict(self, sd: dict):
         if sd.get("format") != "dltb-engine-v1":
@@ -270,6 +301,8 @@ class Engine(ParamRuntime):
         self.seed.state = int(sd["seed_state"])
         self.seed.value = self.seed.state
         self.opt.load_state_dict(sd["optimizer"])
+        if self.scaler is not None and sd.get("loss_scaler") is not None:
+            self.scaler.load_state_dict(sd["loss_scaler"])
         self._after_param_load()
 
     def _after_param_load(self):

@@ -70,7 +70,7 @@ class ReplicatedEngine(Engine):
         # ranks in fp32, and AdamW reads the fp32 sum (2x the wire bytes, no bf16 rounding per hop)
         self.comm_f32 = None
         if self.stage == 0 and self.world > 1 and cfg.extra.get("grad_comm_dtype") == "fp32" \
-                and dt != torch.float32:
+                and dt != torch.float32:    # (fp16 grads are S-scaled: their fp32 sum cannot overflow)
             self.comm_f32 = torch.zeros(L.total, dtype=torch.float32, device=dev)
         for s in L.slots.values():
             p = s.unit.params[s.index]
@@ -263,10 +263,7 @@ class ReplicatedEngine(Engine):
         return self.rs_out if self.world > 1 else self.flat_grad
 
     def _update(self, lr):
-        g = self._owner_grad()
-        extra = 1.0 / (self.world * self.accum)
-        gscale = self._clip_coef([g], extra, sharded=self.stage >= 1)
-        self.opt.step(g, lr, gscale)
+        self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
 
     def _deferred_optimizer_step(self, lr):
         self._update(lr)

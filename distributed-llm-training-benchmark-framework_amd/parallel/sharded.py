@@ -354,9 +354,7 @@ class ShardedEngine(Engine):
 
     def _optimizer_step(self, lr):
         g = self.acc if self.acc is not None else self.rs_out
-        extra = 1.0 / (self.world * self.accum)
-        gscale = self._clip_coef([g], extra, sharded=True)
-        self.opt.step(g, lr, gscale)
+        self._apply_update(g, lr, 1.0 / (self.world * self.accum), sharded=True)
         for grp in self.groups:                   # gathered copies are stale now
             self._release(grp)
         pc = self.p_layout.owner_numel

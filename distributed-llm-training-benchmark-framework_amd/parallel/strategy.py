@@ -114,6 +114,8 @@ def engine_config(strategy: str, grad_accum: int = 1, semantics: str = "referenc
         cfg.prefetch = 0 if bp in ("none", "false", "no") else 1
         if fc.get("mixed_precision") is False and fc.get("param_dtype") == "float32":
             cfg.compute_dtype = torch.float32
+    if compute_dtype == torch.float16:
+        cfg.extra["loss_scaling"] = True     # GradScaler semantics (train_harness.py:334-335, 371-376)
     cfg.extra["semantics"] = semantics
     for k, v in (overrides or {}).items():
         setattr(cfg, k, v)

@@ -68,7 +68,7 @@ def run_case(name, spec, world, rank, device, a):
             over["persistence_threshold"] = spec["persist"]
     cfg = engine_config(spec["strategy"], a.accum, "uniform", None, fc, bucket_mb=a.bucket_mb,
                         overrides=over, grad_reduce=spec.get("grad_reduce", "micro"))
-    cfg.extra["grad_comm_dtype"] = spec.get("grad_comm_dtype", "bf16")
+    cfg.extra["grad_comm_dtype"] = spec.get("grad_comm_dtype", "compute")
     eng = make_engine(model, cfg, device)
     eng.train()
     g = torch.Generator().manual_seed(123)

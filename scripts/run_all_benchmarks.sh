@@ -5,7 +5,10 @@
 #     summary/xgmi_buckets.json (and profiles/xgmi_buckets.json on real GPUs), which
 #     comm/topology.py reads to size the gradient buckets of every following run.
 #  2. Each config: launch (torchrun) -> collect -> failure bookkeeping.  Rows (STRATS):
-#       ddp fsdp zero2 zero3      the reference's four strategies, reference semantics
+#       ddp fsdp zero2 zero3      the reference's four strategies, reference semantics and precision
+#                                 (DDP / FSDP: fp16 + dynamic loss scaling, DDP fp32 all-reduce;
+#                                 ZeRO: bf16 as the DS configs)
+#       ddp_bf16 fsdp_bf16        DDP / FSDP in bf16 (bf16 gradient communication)
 #       fsdp_root                 FSDP with the reference's effective layout: ONE root FlatParameter
 #                                 (configs/fsdp/fsdp_reference_root.yaml)
 #       ddp_uniform fsdp_uniform  DDP / FSDP with ZeRO semantics (grad-accum 4, clip 1.0, WarmupLR)
@@ -21,7 +24,7 @@ set -uo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 RESULTS="${1:-$ROOT/results}"
 STEPS="${STEPS:-100}"; SEQ="${SEQ:-2048}"; TIER="${TIER:-A}"; TIMEOUT="${TIMEOUT:-900}"
-STRATS="${STRATS:-ddp fsdp zero2 zero3 fsdp_root ddp_uniform fsdp_uniform}"
+STRATS="${STRATS:-ddp fsdp zero2 zero3 fsdp_root ddp_bf16 fsdp_bf16 ddp_uniform fsdp_uniform}"
 NGPU="${FORCE_NPROC:-$(python3 -c "import torch; print(torch.cuda.device_count())" 2>/dev/null || echo 0)}"
 read -r -a HX <<< "${HARNESS_EXTRA:-}"
 WS_LIST="${WS_LIST:-1 2 4 8}"
@@ -66,6 +69,7 @@ variant() {   # row name -> "engine strategy|extra harness flags"
     ddp|fsdp|zero2|zero3) echo "$1|" ;;
     fsdp_root) echo "fsdp|--fsdp-config $ROOT/configs/fsdp/fsdp_reference_root.yaml --strategy-label fsdp_root" ;;
     ddp_uniform|fsdp_uniform) echo "${1%_uniform}|--accum-semantics uniform --strategy-label $1" ;;
+    ddp_bf16|fsdp_bf16) echo "${1%_bf16}|--dtype bf16 --strategy-label $1" ;;
     zero1) echo "zero2|--grad-reduce window --strategy-label zero1" ;;
     *) echo "" ;;
   esac

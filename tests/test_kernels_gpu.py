@@ -400,6 +400,15 @@ def test_attention(B, T, Hq, Hkv, D, causal, p):
         close(a, b, 5e-2, 5e-2, "fused-delta d" + name)
 
 
+@pytest.mark.parametrize("B,T,Hq,Hkv,D,causal,p", [
+    (1, 2048, 16, 16, 64, False, 0.1),     # TinyGPT-A bench shape (non-causal, dropout 0.1)
+    (1, 4096, 32, 8, 128, True, 0.0),      # Mistral-7B shape: causal GQA 32/8, D=128, gsplit dK/dV
+])
+def test_attention_full_shape_fwd_bwd(B, T, Hq, Hkv, D, causal, p):
+    """The shapes the benchmarks run, forward AND backward, against the fp32 reference."""
+    test_attention(B, T, Hq, Hkv, D, causal, p)
+
+
 def test_attention_tinygpt_shape():
     """Tier-A shape: T=2048, 16 heads, D=64, non-causal, dropout 0.1 (fwd only vs fp32)."""
     C = ext()
