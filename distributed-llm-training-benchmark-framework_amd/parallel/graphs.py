@@ -59,6 +59,10 @@ class GraphedStep:
         self.static_tgt = None
         self.n = 0
         self.disabled = False
+        if getattr(engine, "_tail_defer", False):
+            # reduce-scatters left in flight across micro-steps would cross graph boundaries
+            engine._drain_all()
+            engine._tail_defer = False
 
     def _eager(self, idx, tgt):
         loss = self.e(idx, tgt)[1]

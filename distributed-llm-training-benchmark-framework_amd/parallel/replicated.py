@@ -112,6 +112,15 @@ class ReplicatedEngine(Engine):
         # block i-1's dropout colpart launch instead of a launch of their own
         self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda") else None
         self._launched = [False] * len(L.buckets)
+        # ZeRO-2 per-micro-step reduce-scatter, world > 1: a micro-step that does not end its window
+        # leaves its buckets' reduce-scatters in flight instead of waiting at the end of backward; the
+        # next backward waits for bucket b (and folds its chunk into the fp32 accumulator) only when it
+        # first writes that bucket's gradient slots, so the tail buckets (block 0, the 70 MB
+        # embedding) reduce under the next forward instead of after the backward.  The window's
+        # last micro-step drains everything before the optimizer.
+        self._tail_defer = (self.stage == 2 and self.world > 1 and self.acc is not None and
+                            bool(cfg.extra.get("defer_tail_reduce", True)))
+        self._rs_inflight = {}   # bucket -> (work, first micro-step of its window)
         nbytes = L.total * (4 if self.comm_f32 is not None else elem)
         if self.world > 1:
             # modelled wire bytes one rank sends per micro-step (ring algorithms): DDP one all-reduce
@@ -180,6 +189,10 @@ class ReplicatedEngine(Engine):
         return self.acquire(unit)
 
     def grad_slot(self, unit, i):
+        if self._rs_inflight:
+            b = self._bucket_of.get(id(unit))
+            if b in self._rs_inflight:
+                self._drain_bucket(b)           # the previous micro-step's reduce-scatter reads this slot
         s = self.layout.slot(unit, i)
         return self.flat_grad[s.offset:s.offset + s.numel].view(s.shape), self._mark(unit, i)
 
@@ -223,9 +236,30 @@ class ReplicatedEngine(Engine):
                 self.comm.all_reduce(c)
             else:
                 self.comm.all_reduce(g)
+        elif self._tail_defer:
+            w = self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g, track=False)
+            self._rs_inflight[b] = (w, self._window_pos == 0)
         else:
             self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g)
         self._launched[b] = True
+
+    def _drain_bucket(self, b):
+        """Wait for bucket ``b``'s reduce-scatter and add its chunk into the fp32 accumulator."""
+        w, first = self._rs_inflight.pop(b)
+        w.wait()
+        bk = self.layout.buckets[b]
+        a = self.acc[bk.owner_start:bk.owner_start + bk.chunk]
+        r = self.rs_out[bk.owner_start:bk.owner_start + bk.chunk]
+        if a.is_cuda:
+            ext().f32_from_bf16_(a, r, not first)
+        elif first:
+            a.copy_(r)
+        else:
+            a += r
+
+    def _drain_all(self):
+        for b in sorted(self._rs_inflight):
+            self._drain_bucket(b)
 
     # ------------------------------------------------------------------ step lifecycle
     def _on_begin_micro(self):
@@ -242,10 +276,12 @@ class ReplicatedEngine(Engine):
                     self._launch(b)
         self._phase("comm_wait_begin")
         self._wait_works()
+        if self._tail_defer and self._is_boundary:
+            self._drain_all()                   # the optimizer reads the window's full sum next
         self._phase("comm_wait_end")
         self._pending = [len(b.units) for b in self.layout.buckets]
         self._launched = [False] * len(self.layout.buckets)
-        if self.stage == 2 and self.acc is not None:
+        if self.stage == 2 and self.acc is not None and not self._tail_defer:
             src = self.rs_out if self.world > 1 else self.flat_grad
             first = self._window_pos == 0
             if self.acc.is_cuda:
@@ -274,6 +310,7 @@ class ReplicatedEngine(Engine):
             self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
 
     def _wait_param_gathers(self):
+        self._drain_all()
         for w in self._ag_pending.values():
             w.wait()
         self._ag_pending.clear()

@@ -1,13 +1,67 @@
-import cProfile, pstats, sys, os, io
-sys.argv = ["bench.py", "--graphs", "off", "--steps", "12", "--warmup", "8"]
-sys.path.insert(0, os.getcwd())
-import runpy
-pr = cProfile.Profile()
-pr.enable()
-try:
-    runpy.run_path("bench.py", run_name="__main__")
-finally:
+#!/usr/bin/env python3
+"""Host-side (Python) cost of an eager TinyGPT-A micro-step: cProfile over K eager steps after
+warm-up, top functions by own time.  Eager execution is what multi-rank runs use, so every
+microsecond of Python per step that exceeds the GPU time is lost wall time.
+
+    python scripts/host_profile.py [--steps 20] [--strategy zero2] [--top 40]
+"""
+import argparse
+import cProfile
+import io
+import os
+import pstats
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import dltb  # noqa: E402,F401
+from dltb.models import build_model, get_model_config  # noqa: E402
+from dltb.parallel import engine_config, make_engine  # noqa: E402
+from dltb.utils.gemm_tuning import setup_tunableop  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--strategy", default="zero2")
+    ap.add_argument("--top", type=int, default=40)
+    a = ap.parse_args()
+    setup_tunableop("auto")
+    torch.manual_seed(0)
+    cfg = get_model_config("A", 2048)
+    with torch.device("cuda"):
+        model = build_model(cfg)
+    eng = make_engine(model, engine_config(a.strategy, 4, "reference"), "cuda:0")
+    eng.train()
+    idx = torch.randint(0, cfg.vocab_size, (1, 2048), device="cuda")
+
+    def step():
+        loss = eng(idx, idx)[1]
+        eng.backward(loss)
+        eng.step()
+
+    for _ in range(8):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    host = (time.perf_counter() - t0) / a.steps
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / a.steps
+    print(f"host enqueue {host * 1e3:.3f} ms/step, wall {wall * 1e3:.3f} ms/step")
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(a.steps):
+        step()
     pr.disable()
+    torch.cuda.synchronize()
     s = io.StringIO()
-    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(35)
-    open("gpurun_out/host_prof.txt", "w").write(s.getvalue())
+    pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(a.top)
+    print(s.getvalue())
+
+
+if __name__ == "__main__":
+    main()
