@@ -30,6 +30,21 @@
 // softmax kernels pay 2 VALU ops per probability for dropout.
 #include <cstdlib>
 
+// DLTB_ATTN_PK=1: the softmax math as packed fp32 (v_pk_fma / v_pk_mul / v_pk_add, two scores per
+// instruction).  Default 0: scalar f32 ops, and the file is built with -fno-slp-vectorize so the
+// compiler does not re-pack them: beside MFMAs a packed f32 op costs far more issue time than the
+// two scalar ops it replaces (MI355X_MICROARCH 'price of one filler beside MFMAs').
+#ifndef DLTB_ATTN_PK
+#define DLTB_ATTN_PK 0
+#endif
+// DLTB_ATTN_PIPE=1: the backward kernels compute S / dP of BOTH 32-row sub-tiles of a
+// 64-row tile before the first softmax, so one sub-tile's MFMAs run under the other's VALU softmax
+// inside the same wave.  Default 0 (sub-tile after sub-tile): measured equal or faster on MI355X
+// (TinyGPT-A dK/dV 56.2-57.2 vs 58.5-59.0 us, profiles/attention_ab_r2.txt).
+#ifndef DLTB_ATTN_PIPE
+#define DLTB_ATTN_PIPE 0
+#endif
+
 #include "common.h"
 #include "mfma_tiles.h"
 
@@ -316,6 +331,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
 #pragma unroll
         for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
       }
+#if DLTB_ATTN_PK
       // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two probabilities per VALU op
       typedef float f32x2 __attribute__((ext_vector_type(2)));
       const f32x2 c2 = {c, c}, nm2 = {-m, -m};
@@ -329,6 +345,18 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
         sacc[n][i + 1] = DROP ? keep_and<16 * n + i + 1>(p[1], mw) : p[1];
       });
       l += ls2[0] + ls2[1];
+#else
+      const float nm = -m;
+      float ls0 = 0.f, ls1 = 0.f;
+      static_for<32>([&](auto J) {
+        constexpr int n = J / 16, i = J % 16;
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][i], c, nm));
+        if constexpr (i & 1) ls1 += p;
+        else ls0 += p;
+        sacc[n][i] = DROP ? keep_and<16 * n + i>(p, mw) : p;
+      });
+      l += ls0 + ls1;
+#endif
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
 #pragma unroll
@@ -583,6 +611,22 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
         }
         const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
         const uint32_t Mv[4] = {M4.x, M4.y, M4.z, M4.w};
+#if !DLTB_ATTN_PK
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          float p = __builtin_amdgcn_exp2f(sa[i] * c);
+          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
+          if (DROP) {     // dS = fma(p keep, dP', p D): the masked probability carries the keep bit
+            const float pdv = __uint_as_float(__float_as_uint(p) & keep_mask_v(Mv[e], jbit));
+            pd[i] = pdv;
+            ds[i] = __builtin_fmaf(pdv, dp[i], p * Dv[e]);
+          } else {
+            pd[i] = p;
+            ds[i] = p * dp[i];
+          }
+        }
+#else
         // packed fp32 (v_pk_mul / v_pk_add): two scores per VALU op, same roundings
         typedef float f32x2 __attribute__((ext_vector_type(2)));
         const f32x2 c2 = {c, c};
@@ -611,6 +655,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
           ds[i] = d[0];
           ds[i + 1] = d[1];
         }
+#endif
       }
     };
     auto accum = [&](int mm, const f32x16& pd, const f32x16& ds) {
@@ -626,10 +671,9 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
       }
     };
     if (t < nT) {
-      if (D == 128 && (!CAUSAL || t * kTile >= k0 + 31)) {
-        // full tile (no mask) at 1 wave / SIMD: both sub-tiles' S/dP first, so the second pair's
-        // MFMAs overlap the first sub-tile's softmax, and its dV/dK MFMAs overlap the second
-        // softmax (at D = 64 more waves per SIMD do that, and the registers are needed for them)
+      if ((D == 128 || DLTB_ATTN_PIPE) && (!CAUSAL || t * kTile >= k0 + 31)) {
+        // full tile (no mask): both sub-tiles' S/dP first, so the second pair's MFMAs overlap the
+        // first sub-tile's softmax, and its dV/dK MFMAs overlap the second softmax
         f32x16 sa0, dp0, sa1, dp1, pd, ds;
         sdp(0, sa0, dp0);
         sdp(1, sa1, dp1);
@@ -841,40 +885,70 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
     const char* vt = kt + TB;
     const uint32_t mw = DROP ? *reinterpret_cast<const uint32_t*>(kt + 2 * TB + wv * 256 + lane * 4) : 0u;
     const int kv0 = t * kTile;
+    // S^T / dP^T of key sub-tile n (32 keys x this wave's 32 queries)
+    auto sdp = [&](int n, f32x16& sa, f32x16& dp) {
+      sa = f32x16{};
+      dp = f32x16{};
+#pragma unroll
+      for (int s = 0; s < D / 16; ++s) {
+        sa = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sa);
+        dp = mfma32(row_frag<D>(vt, 32 * n + r, 2 * s + h), of[s], dp);
+      }
+    };
+    // softmax / dS of sub-tile n and dQ^T += K^T dS^T
+    auto fin = [&](int n, const f32x16& sa, const f32x16& dp) {
+      const bool diag = CAUSAL && kv0 + 32 * n + 31 > q0;
+      f32x16 ds;
+#if !DLTB_ATTN_PK
+      static_for<16>([&](auto I) {
+        constexpr int i = I;
+        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], c, nlc));
+        if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
+        const float dpv = DROP ? (n == 0 ? keep_and<i>(dp[i], mw) : keep_and<16 + i>(dp[i], mw)) : dp[i];
+        ds[i] = p * (dpv + nd);
+      });
+#else
+      // packed fp32 (v_pk_fma / v_pk_add / v_pk_mul): two scores per VALU op, same roundings
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 c2 = {c, c}, nl2 = {nlc, nlc}, nd2 = {nd, nd};
+      static_for<8>([&](auto J) {
+        constexpr int i = 2 * J;
+        const f32x2 x = __builtin_elementwise_fma(f32x2{sa[i], sa[i + 1]}, c2, nl2);
+        f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+        if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p[0] = 0.f;
+        if (diag && kv0 + 32 * n + ((i + 1) & 3) + 8 * ((i + 1) >> 2) + 4 * h > qi) p[1] = 0.f;
+        const f32x2 dpv = DROP ? (n == 0 ? f32x2{keep_and<i>(dp[i], mw), keep_and<i + 1>(dp[i + 1], mw)}
+                                         : f32x2{keep_and<16 + i>(dp[i], mw), keep_and<17 + i>(dp[i + 1], mw)})
+                               : f32x2{dp[i], dp[i + 1]};
+        const f32x2 d = p * (dpv + nd2);
+        ds[i] = d[0];
+        ds[i + 1] = d[1];
+      });
+#endif
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bfx8 sf = pack_frag<D>(ds, s2);
+#pragma unroll
+        for (int dt = 0; dt < NACC; ++dt)
+          dq[dt] = mfma32(tr_frag<D>(kt, 32 * n + 16 * s2, dt * 32, lane), sf, dq[dt]);
+      }
+    };
     if (t < nt) {
+      if (DLTB_ATTN_PIPE && D == 64 && (!CAUSAL || kv0 + kTile - 1 <= q0)) {   // (D = 128: registers)
+        // full tile: both sub-tiles' S / dP first, so sub-tile 1's MFMAs run under sub-tile 0's
+        // softmax and sub-tile 0's dQ MFMAs under sub-tile 1's softmax
+        f32x16 sa0, dp0, sa1, dp1;
+        sdp(0, sa0, dp0);
+        sdp(1, sa1, dp1);
+        fin(0, sa0, dp0);
+        fin(1, sa1, dp1);
+      } else {
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        if (CAUSAL && kv0 + 32 * n > q0 + 31) continue;
-        f32x16 sa = f32x16{}, dp = f32x16{};
-#pragma unroll
-        for (int s = 0; s < D / 16; ++s) {
-          sa = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sa);
-          dp = mfma32(row_frag<D>(vt, 32 * n + r, 2 * s + h), of[s], dp);
-        }
-        const bool diag = CAUSAL && kv0 + 32 * n + 31 > q0;
-        f32x16 ds;
-        // packed fp32 (v_pk_fma / v_pk_add / v_pk_mul): two scores per VALU op, same roundings
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        const f32x2 c2 = {c, c}, nl2 = {nlc, nlc}, nd2 = {nd, nd};
-        static_for<8>([&](auto J) {
-          constexpr int i = 2 * J;
-          const f32x2 x = __builtin_elementwise_fma(f32x2{sa[i], sa[i + 1]}, c2, nl2);
-          f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-          if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p[0] = 0.f;
-          if (diag && kv0 + 32 * n + ((i + 1) & 3) + 8 * ((i + 1) >> 2) + 4 * h > qi) p[1] = 0.f;
-          const f32x2 dpv = DROP ? (n == 0 ? f32x2{keep_and<i>(dp[i], mw), keep_and<i + 1>(dp[i + 1], mw)}
-                                           : f32x2{keep_and<16 + i>(dp[i], mw), keep_and<17 + i>(dp[i + 1], mw)})
-                                 : f32x2{dp[i], dp[i + 1]};
-          const f32x2 d = p * (dpv + nd2);
-          ds[i] = d[0];
-          ds[i + 1] = d[1];
-        });
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bfx8 sf = pack_frag<D>(ds, s2);
-#pragma unroll
-          for (int dt = 0; dt < NACC; ++dt)
-            dq[dt] = mfma32(tr_frag<D>(kt, 32 * n + 16 * s2, dt * 32, lane), sf, dq[dt]);
+        for (int n = 0; n < 2; ++n) {
+          if (CAUSAL && kv0 + 32 * n > q0 + 31) continue;
+          f32x16 sa, dp;
+          sdp(n, sa, dp);
+          fin(n, sa, dp);
         }
       }
     }
