@@ -1,0 +1,200 @@
+// hipBLASLt extension-API GEMMs with tuned (solution, splitK, wgm) triples -- see blaslt.h.
+//
+// Host code only (no kernels of its own): it drives the hipBLASLt library PyTorch ships (the
+// extension resolves libhipblaslt.so.1 to the copy torch already loaded), so the solution indices
+// of a tuning table are those of the kernel library torch's own GEMMs use.  Only entry points that
+// library exports are called (it predates GemmInstance::setMaxWorkspaceBytes: the workspace limit
+// is enforced here, from isAlgoSupported's requirement).
+#include "blaslt.h"
+
+#include <hipblaslt/hipblaslt-ext.hpp>
+#include <hipblaslt/hipblaslt.h>
+
+#include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <tuple>
+
+namespace {
+
+constexpr size_t kWorkspace = 64ull << 20;    // split-K partials of the largest tuned product fit
+
+const float kOne = 1.f, kZero = 0.f;           // host alpha / beta (read when arguments are built)
+
+std::mutex g_mu;
+
+hipblasLtHandle_t handle() {
+  static hipblasLtHandle_t h = [] {
+    hipblasLtHandle_t x = nullptr;
+    if (hipblasLtCreate(&x) != HIPBLAS_STATUS_SUCCESS) throw std::runtime_error("hipblasLtCreate failed");
+    return x;
+  }();
+  return h;
+}
+
+void* workspace() {
+  static void* ws = [] {
+    void* p = nullptr;
+    if (hipMalloc(&p, kWorkspace) != hipSuccess) throw std::runtime_error("blaslt workspace alloc failed");
+    return p;
+  }();
+  return ws;
+}
+
+hipblasOperation_t op(int t) { return t ? HIPBLAS_OP_T : HIPBLAS_OP_N; }
+hipDataType dtype(const BltProblem& p) { return p.f16 ? HIP_R_16F : HIP_R_16BF; }
+
+std::unique_ptr<hipblaslt_ext::Gemm> make_gemm(const BltProblem& p, const void* A, const void* B, void* C,
+                                               const void* bias) {
+  const hipDataType dt = dtype(p);
+  auto g = std::make_unique<hipblaslt_ext::Gemm>(handle(), op(p.opA), op(p.opB), dt, dt, dt, dt,
+                                                  HIPBLAS_COMPUTE_32F);
+  hipblaslt_ext::GemmEpilogue epi;
+  hipblaslt_ext::GemmInputs in;
+  if (p.bias) {
+    epi.setMode(HIPBLASLT_EPILOGUE_BIAS);
+    epi.setBiasDataType(dt);
+    in.setBias(bias);
+  }
+  in.setA(A);
+  in.setB(B);
+  in.setC(C);
+  in.setD(C);
+  in.setAlpha(&kOne);
+  in.setBeta(p.beta1 ? &kOne : &kZero);
+  hipblaslt_ext::GemmProblemType pt(op(p.opA), op(p.opB), dt, dt, dt, dt, HIPBLAS_COMPUTE_32F);
+  if (g->setProblem(p.m, p.n, p.k, p.batch, p.lda, p.ldb, p.ldc, p.ldc, p.sa, p.sb, p.sc, p.sc, epi, in, pt) !=
+      HIPBLAS_STATUS_SUCCESS)
+    return nullptr;
+  return g;
+}
+
+std::vector<hipblasLtMatmulHeuristicResult_t> all_algos(const BltProblem& p) {
+  std::vector<hipblasLtMatmulHeuristicResult_t> r;
+  const hipDataType dt = dtype(p);
+  hipblaslt_ext::getAllAlgos(handle(), hipblaslt_ext::GemmType::HIPBLASLT_GEMM, op(p.opA), op(p.opB), dt, dt,
+                             dt, dt, HIPBLAS_COMPUTE_32F, r);
+  return r;
+}
+
+bool algo_of(int index, hipblasLtMatmulAlgo_t& algo) {
+  std::vector<int> idx{index};
+  std::vector<hipblasLtMatmulHeuristicResult_t> r;
+  if (hipblaslt_ext::getAlgosFromIndex(handle(), idx, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) return false;
+  algo = r[0].algo;
+  return true;
+}
+
+hipblaslt_ext::GemmTuning tuning_of(int splitk, int wgm) {
+  hipblaslt_ext::GemmTuning t;
+  t.setSplitK((uint16_t)splitk);
+  t.setWgm((int16_t)wgm);
+  return t;
+}
+
+// <0: unsupported; else mean microseconds per call over `iters`
+float time_one(hipblaslt_ext::Gemm& g, hipblasLtMatmulAlgo_t algo, int splitk, int wgm, int iters,
+               hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+  auto t = tuning_of(splitk, wgm);
+  size_t need = 0;
+  if (g.isAlgoSupported(algo, t, need) != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) return -1.f;
+  if (g.initialize(algo, t, workspace(), true, st) != HIPBLAS_STATUS_SUCCESS) return -1.f;
+  for (int i = 0; i < 2; ++i)
+    if (g.run(st) != HIPBLAS_STATUS_SUCCESS) return -1.f;
+  hipEventRecord(e0, st);
+  for (int i = 0; i < iters; ++i) g.run(st);
+  hipEventRecord(e1, st);
+  hipEventSynchronize(e1);
+  float ms = 0.f;
+  hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1000.f / iters;
+}
+
+// Initialised problems keyed by shape, tuning AND operand pointers: the model's GEMM operands live
+// in preallocated (layer-strided) buffers, so every call site repeats its pointers step after step
+// and, after the first step, is a bare kernel launch (also inside HIP-graph capture).
+using Key = std::tuple<int, int, long, long, long, long, long, long, long, long, long, long, int, int, int, int, int,
+                       int, const void*, const void*, const void*, const void*>;
+constexpr size_t kMaxCached = 8192;
+
+Key key_of(const BltProblem& p, int algo, int splitk, int wgm, const void* A, const void* B, const void* C,
+           const void* bias) {
+  return Key{p.opA, p.opB, p.m, p.n, p.k, p.batch, p.lda, p.ldb, p.ldc, p.sa, p.sb, p.sc, p.f16, p.beta1,
+             p.bias, algo, splitk, wgm, A, B, C, bias};
+}
+
+std::map<Key, std::unique_ptr<hipblaslt_ext::Gemm>>& cache() {
+  static std::map<Key, std::unique_ptr<hipblaslt_ext::Gemm>> c;
+  return c;
+}
+
+}  // namespace
+
+std::vector<BltResult> dltb_blaslt_sweep(const BltProblem& p, const void* A, const void* B, void* C,
+                                         const void* bias, int iters,
+                                         const std::vector<int>& splitks, const std::vector<int>& wgms,
+                                         int refine, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::vector<BltResult> out;
+  auto g = make_gemm(p, A, B, C, bias);
+  if (!g) return out;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  auto algos = all_algos(p);
+  std::vector<std::pair<float, size_t>> base;
+  for (size_t i = 0; i < algos.size(); ++i) {
+    const float us = time_one(*g, algos[i].algo, 0, 0, iters, st, e0, e1);
+    if (us < 0) continue;
+    base.push_back({us, i});
+    out.push_back({hipblaslt_ext::getIndexFromAlgo(algos[i].algo), 0, 0, us,
+                   hipblaslt_ext::getSolutionNameFromAlgo(handle(), algos[i].algo)});
+  }
+  std::sort(base.begin(), base.end());
+  if ((int)base.size() > refine) base.resize(refine);
+  for (auto& b : base) {
+    auto& a = algos[b.second];
+    for (int sk : splitks)
+      for (int wg : wgms) {
+        if (sk == 0 && wg == 0) continue;
+        const float us = time_one(*g, a.algo, sk, wg, iters, st, e0, e1);
+        if (us < 0) continue;
+        out.push_back({hipblaslt_ext::getIndexFromAlgo(a.algo), sk, wg, us,
+                       hipblaslt_ext::getSolutionNameFromAlgo(handle(), a.algo)});
+      }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  std::sort(out.begin(), out.end(), [](const BltResult& x, const BltResult& y) { return x.us < y.us; });
+  return out;
+}
+
+int dltb_blaslt_run(const BltProblem& p, const void* A, const void* B, void* C, const void* bias, int algo,
+                    int splitk, int wgm, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto& c = cache();
+  const Key key = key_of(p, algo, splitk, wgm, A, B, C, bias);
+  auto it = c.find(key);
+  if (it == c.end()) {
+    hipblasLtMatmulAlgo_t a;
+    if (!algo_of(algo, a)) return -1;
+    auto g = make_gemm(p, A, B, C, bias);
+    if (!g) return -2;
+    auto t = tuning_of(splitk, wgm);
+    size_t need = 0;
+    if (g->isAlgoSupported(a, t, need) != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) return -3;
+    if (g->initialize(a, t, workspace(), true, st) != HIPBLAS_STATUS_SUCCESS) return -4;
+    if (c.size() >= kMaxCached) c.clear();    // transient (allocator-churned) pointers: start over
+    it = c.emplace(key, std::move(g)).first;
+  }
+  return it->second->run(st) == HIPBLAS_STATUS_SUCCESS ? 0 : -5;
+}
+
+std::string dltb_blaslt_name(int algo) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipblasLtMatmulAlgo_t a;
+  if (!algo_of(algo, a)) return "";
+  return hipblaslt_ext::getSolutionNameFromAlgo(handle(), a);
+}

@@ -1,11 +1,14 @@
 """Device dispatch of the dltb ops: GPU tensors run the gfx950 HIP kernels of ``dltb._C``
 (raising if the extension is missing), CPU tensors run the torch references of :mod:`.ref`.
 
-GEMMs are plain ``torch`` matmuls (hipBLASLt on ROCm); gradient-producing GEMMs write straight
-into the engine's flat gradient slots (``out=`` / ``addmm_``) so no gradient is ever copied.
+GEMMs run on hipBLASLt: the problems of the shipped tuning table through the extension API with
+their tuned (solution, split-K, wgm) triple (:mod:`.blaslt`), everything else as plain ``torch``
+matmuls (TunableOp); gradient-producing GEMMs write straight into the engine's flat gradient slots
+(``out=`` / ``addmm_``) so no gradient is ever copied.
 """
 import torch
 
+from . import blaslt as _blt
 from . import ref
 from ._ext import ext
 
@@ -315,7 +318,18 @@ def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal,
 
 
 # ------------------------------------------------------------------------------ linear
+def _tuned(a, b, bias=None):
+    """a @ b (+ bias) through the tuned hipBLASLt table, or None when the problem is not in it."""
+    if not (_blt.active() and a.is_cuda):
+        return None
+    y = a.new_empty(a.shape[0], b.shape[1])
+    return y if _blt.mm(a, b, y, False, bias) else None
+
+
 def linear_fwd(x2d, w, b=None):
+    y = _tuned(x2d, w.t(), b)
+    if y is not None:
+        return y
     if b is None:
         return torch.mm(x2d, w.t())
     return torch.addmm(b, x2d, w.t())
@@ -323,14 +337,14 @@ def linear_fwd(x2d, w, b=None):
 
 def linear_dgrad(dy2d, w, wt=None):
     """dX = dY W; with a cached contiguous W^T the product runs as dY (W^T)^T (hipBLASLt NT form)."""
-    if wt is not None:
-        return torch.mm(dy2d, wt.t())
-    return torch.mm(dy2d, w)
+    rhs = wt.t() if wt is not None else w
+    y = _tuned(dy2d, rhs)
+    return y if y is not None else torch.mm(dy2d, rhs)
 
 
 def linear_wgrad(dy2d, x2d, dw, db, accumulate):
     """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy)."""
-    if dw is not None:
+    if dw is not None and not _blt.mm(dy2d.t(), x2d, dw, accumulate):
         if accumulate:
             dw.addmm_(dy2d.t(), x2d)
         else:

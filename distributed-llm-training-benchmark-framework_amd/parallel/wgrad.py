@@ -26,6 +26,8 @@ from typing import Dict, List, Optional
 
 import torch
 
+from ..ops import blaslt as _blt
+
 
 def strided_batch(ts: List[torch.Tensor], out: bool = False) -> Optional[torch.Tensor]:
     """A [n, *shape] view covering the equally spaced same-shape 2-D tensors ``ts`` (in order) of
@@ -78,14 +80,18 @@ class WgradQueue:
             DY = strided_batch([it[0] for it in items])
             X = strided_batch([it[1] for it in items])
             if DW is not None and DY is not None and X is not None:
-                if acc:
+                if _blt.mm(DY.transpose(1, 2), X, DW, acc):
+                    pass
+                elif acc:
                     DW.baddbmm_(DY.transpose(1, 2), X)
                 else:
                     torch.bmm(DY.transpose(1, 2), X, out=DW)
                 self.batched_calls += 1
                 return
         for dy, x, dw in items:                              # not equally spaced: one GEMM each
-            if acc:
+            if _blt.mm(dy.t(), x, dw, acc):
+                pass
+            elif acc:
                 dw.addmm_(dy.t(), x)
             else:
                 torch.mm(dy.t(), x, out=dw)

@@ -9,6 +9,11 @@ M = B*T = 2048 training shapes, so the framework ships TunableOp results measure
     mode "tune" : benchmark every hipBLASLt/rocBLAS candidate for each new GEMM signature and write
                   the results file (run once on one GPU; ``scripts/tune_gemms.sh``)
     mode "off"  : library defaults
+
+On top of TunableOp's solution choice, "use" also loads the hipBLASLt extension-API table
+(``configs/blaslt/*.csv``, :mod:`dltb.ops.blaslt`): per exact problem a solution plus run-time
+split-K and workgroup mapping, measured faster than TunableOp's pick by ``scripts/tune_blaslt.py``.
+The returned mode string then reads ``use+blaslt<n entries>``.
 """
 import os
 
@@ -41,6 +46,11 @@ def setup_tunableop(mode: str = "auto", path: str = None, verbose: bool = False)
         tn.read_file(path)
     if verbose:
         print(f"[dltb] TunableOp {mode}: {path}", flush=True)
+    if mode == "use":
+        from ..ops import blaslt
+        n = blaslt.load(verbose=verbose)
+        if n:
+            return f"use+blaslt{n}"
     return mode
 
 
