@@ -153,7 +153,11 @@ class _BlockFn(torch.autograd.Function):
         s = [rt.grad_slot(unit, j) for j in range(12)]
         lb = ctx.lb
 
-        def wgrad(j, dy, xin):             # dW_j (+)= dy^T xin: now, or queued and batched by the engine
+        def wgrad(j, dy, xin, names):      # dW_j (+)= dy^T xin: now, or queued and batched by the engine
+            if lb is not None and lb.window:    # window-wide: once, at the last micro-step, all tokens
+                if lb.full is not None:
+                    rt.wgrad(unit, j, getattr(lb.full, names[0]), getattr(lb.full, names[1]), s[j][0], False)
+                return
             rt.wgrad(unit, j, dy, xin, s[j][0], s[j][1])
 
         # the 8 bias / LayerNorm column sums: fused partials, reduced by ONE launch per block (or,
@@ -163,21 +167,21 @@ class _BlockFn(torch.autograd.Function):
         # MLP
         dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
                                  out=lb and lb.dm)
-        wgrad(10, dm, g)
+        wgrad(10, dm, g, ("dm", "g"))
         dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
         df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
-        wgrad(8, df, h2)
+        wgrad(8, df, h2, ("df", "h2"))
         dh2 = F_.linear_dgrad(df, w1, rt.weight_t(unit, 8, w1))
         dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False,
                           red, bias=("dx", s[5][0], s[5][1]), dx_out=lb and lb.dx1)
         # attention
-        wgrad(4, dx1, o)
+        wgrad(4, dx1, o, ("dx1", "o"))
         do = F_.linear_dgrad(dx1, wo, rt.weight_t(unit, 4, wo))
         dqkv = torch.empty_like(qkv) if lb is None else lb.dqkv
         F_.attn_bwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], o, do, lse, amask,
                     dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
-        wgrad(2, dqkv, h1)
+        wgrad(2, dqkv, h1, ("dqkv", "h1"))
         dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False,
                          red, bias=(dqkv, s[3][0], s[3][1]))
@@ -305,30 +309,43 @@ class TinyGPT(nn.Module):
 
     def _prepare_layer_buffers(self, N, like):
         """Under an engine that batches weight gradients (``rt.defer_wgrad``), the GEMM operands of
-        every block's dW products live in layer-strided buffers [L, N, k] -- one row per block, in
+        every block's dW products live in layer-strided buffers [L, R*N, k] -- one row per block, in
         the order of the blocks' gradient slots in the flat buffer -- so a group of blocks is one
         strided-batched GEMM (parallel/wgrad.py); the row order follows the engine's slot order
         (``rt.wgrad_rows_reversed``).  X: ln_1 / ln_2 outputs, attention output, GELU
-        output; dY: dqkv, d(x1), d(fc1 pre-activation), d(fc2 output).  ~1 GB at TinyGPT-A."""
+        output; dY: dqkv, d(x1), d(fc1 pre-activation), d(fc2 output).  R = 1, or the accumulation
+        window when the engine takes window-wide weight gradients (``rt.wgrad_window()``): micro-step
+        m then writes token rows [m*N, (m+1)*N) and the last one hands over all R*N rows.
+        ~1 GB per window row at TinyGPT-A."""
         if not (getattr(self.rt, "defer_wgrad", False) and self.training and torch.is_grad_enabled()):
             self._lbufs, self._lbuf_key = None, None
             return
+        win = self.rt.wgrad_window()
+        pos, R = win if win is not None else (0, 1)
         L, d, F = self.cfg.n_layer, self.cfg.n_embd, 4 * self.cfg.n_embd
-        key = (L, N, d, like.dtype, like.device)
+        key = (L, N, R, d, like.dtype, like.device)
         if self._lbuf_key != key:
-            mk = lambda k: torch.empty(L, N, k, dtype=like.dtype, device=like.device)  # noqa: E731
+            self._lbufs = None                       # free the old set before allocating the new one
+            mk = lambda k: torch.empty(L, R * N, k, dtype=like.dtype, device=like.device)  # noqa: E731
             self._lbufs = SimpleNamespace(h1=mk(d), o=mk(d), h2=mk(d), g=mk(F), dqkv=mk(3 * d), dx1=mk(d),
                                           df=mk(F), dm=mk(d))
             self._lbuf_key = key
+        self._lbuf_win = (pos, R, N)
         self._lbuf_on = True
 
     def layer_buffer(self, i):
-        """Views of block ``i``'s row of the layer-strided buffers, or None (immediate dW)."""
+        """Views of block ``i``'s row of the layer-strided buffers (this micro-step's token rows), or
+        None (immediate dW).  ``window``: dW is window-wide; ``full`` (at the window's last
+        micro-step, else None): the row's views over all of the window's tokens."""
         b = self._lbufs
         if b is None or not getattr(self, "_lbuf_on", False):
             return None
         r = self.cfg.n_layer - 1 - i if getattr(self.rt, "wgrad_rows_reversed", True) else i
-        return SimpleNamespace(**{k: v[r] for k, v in vars(b).items()})
+        pos, R, N = self._lbuf_win
+        out = SimpleNamespace(**{k: v[r, pos * N:(pos + 1) * N] for k, v in vars(b).items()})
+        out.window = R > 1
+        out.full = SimpleNamespace(**{k: v[r] for k, v in vars(b).items()}) if (R > 1 and pos == R - 1) else None
+        return out
 
     def forward(self, idx, targets=None, return_logits=False):
         B, T = idx.shape

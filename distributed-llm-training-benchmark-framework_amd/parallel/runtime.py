@@ -91,6 +91,13 @@ class ParamRuntime:
     # (backward-ordered replicated layouts); the model's layer-strided buffers follow it
     wgrad_rows_reversed = True
 
+    def wgrad_window(self):
+        """(position, accum) when the engine consumes gradients only at the accumulation-window
+        boundary and wants the window's weight gradients as ONE product per parameter over all its
+        micro-steps' tokens (the model then keeps every micro-step's GEMM operands in its layer
+        buffers and hands over full-window views at the last micro-step); None otherwise."""
+        return None
+
     def grad_reducer(self):
         """A column-sum reducer shared by every block's backward (flushed by the engine once per
         backward), or None: each block reduces its own bias / norm-weight sums before it reports

@@ -3,6 +3,7 @@ five; the side-stream, mask-stream, overlapped-optimizer, standalone-dropout and
 dropout-backward paths were measured neutral or slower and deleted):
 
 * DLTB_GRAPHS (``--graphs``)      x  DLTB_BATCH_WGRAD (``batch_wgrad``)   x  replicated / sharded
+* DLTB_WINDOW_WGRAD (``window_wgrad``, window-wide dW at world 1)  x  DLTB_GRAPHS, replicated
 * DLTB_DEFER_OPT                  -- world > 1 only: tests/test_multirank_gpu.py runs ZeRO-1/2 both ways
 * DLTB_DKDV_GSPLIT                -- causal GQA dK/dV head split, forced off vs auto, below
 * DLTB_COMM_HIGH_PRIORITY         -- an RCCL stream priority (no effect on results; needs >1 GPU)
@@ -34,6 +35,15 @@ def test_toggle_matrix(strategy, graphed, batch_wgrad):
         _BASE[strategy] = _run(strategy, False, windows=2, extra={"batch_wgrad": True})
     l1, s1 = _run(strategy, graphed, windows=2, extra={"batch_wgrad": batch_wgrad})
     l0, s0 = _BASE[strategy]
+    _close(l0, s0, l1, s1)
+
+
+@pytest.mark.parametrize("graphed", [False, True])
+def test_window_wgrad_off_matches(graphed):
+    if "zero2" not in _BASE:
+        _BASE["zero2"] = _run("zero2", False, windows=2, extra={"batch_wgrad": True})
+    l1, s1 = _run("zero2", graphed, windows=2, extra={"batch_wgrad": True, "window_wgrad": False})
+    l0, s0 = _BASE["zero2"]
     _close(l0, s0, l1, s1)
 
 

@@ -79,3 +79,31 @@ def test_engines_batch_tinygpt_wgrads(strategy):
         out.append(e.full_state_dict())
     for n in out[0]:
         assert torch.allclose(out[0][n], out[1][n], atol=2e-5), n     # GEMM summation order only
+
+
+@pytest.mark.parametrize("strategy,stage", [("zero2", None), ("zero2", 1), ("ddp", None)])
+def test_window_wide_wgrad_matches_per_micro(strategy, stage):
+    """World 1 (and window-reduced paths): the window's dW as ONE product over all its micro-steps'
+    tokens (layer buffers hold accum x tokens rows) trains like per-micro-step products."""
+    out = []
+    for window in (True, False):
+        torch.manual_seed(0)
+        m = TinyGPT(get_model_config("tiny", 16, dropout=0.0))
+        cfg = engine_config(strategy, 3, "uniform")
+        cfg.extra["window_wgrad"] = window
+        if stage is not None:
+            cfg.zero_stage = stage
+        e = make_engine(m, cfg, "cpu")
+        assert e._window_wgrad == window
+        e.train()
+        g = torch.Generator().manual_seed(1)
+        for _ in range(6):
+            x = torch.randint(0, 128, (2, 16), generator=g)
+            loss = e(x, x)[1]
+            e.backward(loss)
+            e.step()
+        rows = m._lbufs.h1.shape[1]
+        assert rows == (3 * 2 * 16 if window else 2 * 16)
+        out.append(e.full_state_dict())
+    for n in out[0]:
+        assert torch.allclose(out[0][n], out[1][n], atol=2e-5), n
