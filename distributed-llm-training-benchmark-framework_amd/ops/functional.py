@@ -342,12 +342,43 @@ def linear_dgrad(dy2d, w, wt=None):
     return y if y is not None else torch.mm(dy2d, rhs)
 
 
+# hipBLASLt runs a product fastest with both operands K-contiguous (1.48-1.52 PFLOP/s on
+# Mistral-7B's [4096 x 4096-28672] shapes); a weight gradient dY^T X has neither (dY^T is an
+# M-contiguous view, X N-contiguous: 1.03-1.04 PFLOP/s), and one K-contiguous side already gives
+# 1.22-1.28 (profiles/gemm_layouts_r2.txt).  So for a large product the SMALLER operand is
+# transposed into a K-contiguous copy first (an LDS-tiled transpose, ~2 x bytes / 3.5 TB/s) when
+# the expected 15 % of the GEMM time pays for it 1.5 times over: the FFN weight gradients of
+# Mistral-7B qualify, TinyGPT-A's (K = tokens >> dims, batched over blocks) do not.
+_WGRAD_GEMM_FLOPS = 1.1e15
+_WGRAD_GAIN = 0.15
+_TRANSPOSE_BPS = 3.5e12
+
+
+def wgrad_operands(dy2d, x2d):
+    """(a, b) with dW = a @ b: (dy^T, x), or with the smaller one replaced by a K-contiguous copy."""
+    a, b = dy2d.t(), x2d
+    if not (dy2d.is_cuda and dy2d.dim() == 2 and dy2d.dtype in (torch.bfloat16, torch.float16)):
+        return a, b
+    K, M = dy2d.shape
+    N = x2d.shape[1]
+    gemm_s = 2.0 * M * N * K / _WGRAD_GEMM_FLOPS
+    small = dy2d if dy2d.numel() <= x2d.numel() else x2d
+    cost_s = 2.0 * small.numel() * small.element_size() / _TRANSPOSE_BPS + 5e-6
+    if _WGRAD_GAIN * gemm_s <= 1.5 * cost_s or not small.is_contiguous() or K % 4 or small.shape[1] % 4:
+        return a, b
+    t = torch.empty(small.shape[1], small.shape[0], dtype=small.dtype, device=small.device)
+    ext().transpose_into(small, t)
+    return (t, b) if small is dy2d else (a, t.t())
+
+
 def linear_wgrad(dy2d, x2d, dw, db, accumulate):
     """dW (+)= dy^T x written straight into the gradient slot; db (+)= colsum(dy)."""
-    if dw is not None and not _blt.mm(dy2d.t(), x2d, dw, accumulate):
-        if accumulate:
-            dw.addmm_(dy2d.t(), x2d)
-        else:
-            torch.mm(dy2d.t(), x2d, out=dw)
+    if dw is not None:
+        a, b = wgrad_operands(dy2d, x2d)
+        if not _blt.mm(a, b, dw, accumulate):
+            if accumulate:
+                dw.addmm_(a, b)
+            else:
+                torch.mm(a, b, out=dw)
     if db is not None:
         colsum_into(dy2d, db, accumulate)

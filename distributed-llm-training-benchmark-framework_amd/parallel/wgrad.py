@@ -27,6 +27,7 @@ from typing import Dict, List, Optional
 import torch
 
 from ..ops import blaslt as _blt
+from ..ops import functional as F_
 
 
 def strided_batch(ts: List[torch.Tensor], out: bool = False) -> Optional[torch.Tensor]:
@@ -89,10 +90,5 @@ class WgradQueue:
                 self.batched_calls += 1
                 return
         for dy, x, dw in items:                              # not equally spaced: one GEMM each
-            if _blt.mm(dy.t(), x, dw, acc):
-                pass
-            elif acc:
-                dw.addmm_(dy.t(), x)
-            else:
-                torch.mm(dy.t(), x, out=dw)
+            F_.linear_wgrad(dy, x, dw, None, acc)
             self.single_calls += 1

@@ -124,4 +124,27 @@ def test_blaslt_graph_capture_and_table_dispatch(tmp_path):
         torch.cuda.synchronize()
         check(y, x.float() @ w.float().t() + bias.float(), "graph replay")
     finally:
-        blaslt.load("none")
+        blaslt.load()                     # back to the shipped table
+
+
+@pytest.mark.parametrize("which", ["x_small", "dy_small"])
+def test_wgrad_transposed_operand(which):
+    """Large weight gradients run with the smaller operand transposed K-contiguous
+    (functional.wgrad_operands); the product equals dy^T x, overwrite and accumulate."""
+    from dltb.ops import functional as F_
+    T = 4096
+    out_f, in_f = (14336, 4096) if which == "x_small" else (4096, 14336)
+    dy, x = rnd(T, out_f), rnd(T, in_f)
+    a, b = F_.wgrad_operands(dy, x)
+    if which == "x_small":
+        assert a.stride() == dy.t().stride() and b.stride(0) == 1          # x^T copy, viewed back
+    else:
+        assert a.is_contiguous() and b.data_ptr() == x.data_ptr()          # dy^T copy
+    want = dy.float().t() @ x.float()
+    dw = torch.empty(out_f, in_f, device="cuda", dtype=BF)
+    F_.linear_wgrad(dy, x, dw, None, False)
+    check(dw, want, "overwrite")
+    F_.linear_wgrad(dy, x, dw, None, True)
+    check(dw, 2 * want, "accumulate")
+    small = F_.wgrad_operands(rnd(2048, 1024), rnd(2048, 1024))             # small product: untouched
+    assert small[1].stride(1) == 1 and not small[0].is_contiguous()
