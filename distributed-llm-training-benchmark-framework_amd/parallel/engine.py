@@ -81,6 +81,10 @@ class Engine(ParamRuntime):
         self._gscale = torch.ones(1, device=self.device, dtype=torch.float32)
         self.comm_bytes_per_step = 0
         self.timers = None               # utils.timers.PhaseTimers while the harness times phases
+        self._cache_wt = False   # subclasses: True where parameters stay resident between steps
+        self._wt = {}            # (unit index, param index) -> (W view, W^T view of a stacked buffer)
+        self._wt_stack = {}      # (param index, shape) -> [units, K, N] buffer of transposes
+        self._wt_epoch = -1      # optimizer step the cached transposes belong to
         model.rt = self
         self._setup()
 
@@ -193,6 +197,51 @@ class Engine(ParamRuntime):
     @property
     def is_boundary(self):
         return self._is_boundary
+
+    # ------------------------------------------------------------------ cached weight transposes
+    def weight_t(self, unit, i, w):
+        """Cached W^T for the NT-form data-gradient GEMM (engines whose parameters stay resident
+        between optimizer steps: replicated ones, sharded ones at world size 1).  The transposes of
+        one parameter kind live in one stacked buffer, one row per unit holding that kind in
+        reversed unit order (the order of the parameters in the flat buffers), so after an
+        optimizer step all of them are refreshed by ONE batched LDS-tiled transpose launch per kind
+        instead of one launch per block."""
+        if not self._cache_wt or w.dim() != 2 or not w.is_cuda:
+            return None
+        if self._wt_epoch != self.opt_steps:
+            self._refresh_weight_t()
+            self._wt_epoch = self.opt_steps
+        key = (unit.index, i)
+        hit = self._wt.get(key)
+        if hit is not None:
+            return hit[1]
+        g = (i, tuple(w.shape))
+        stack = self._wt_stack.get(g)
+        # one row per unit holding a parameter of this kind, in reversed unit order
+        rows = [u.index for u in reversed(self.model.units()) if len(u.shapes) > i and u.shapes[i] == g[1]]
+        if stack is None:
+            stack = torch.empty((len(rows), w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+            self._wt_stack[g] = stack
+        wt = stack[rows.index(unit.index)]
+        ext().transpose_into(w, wt)          # first use: transpose now
+        self._wt[key] = (w, wt)
+        return wt
+
+    def _refresh_weight_t(self):
+        from .wgrad import strided_batch
+        groups = {}
+        for (uidx, i), (w, wt) in self._wt.items():
+            groups.setdefault((i, tuple(w.shape)), []).append((w, wt))
+        C = ext()
+        for items in groups.values():
+            items.sort(key=lambda it: it[1].data_ptr())
+            W = strided_batch([it[0] for it in items])
+            WT = strided_batch([it[1] for it in items], out=True)
+            if W is not None and WT is not None and len(items) > 1:
+                C.transpose_batched(items[0][0], items[0][1], len(items), W.stride(0), WT.stride(0))
+            else:
+                for w, wt in items:
+                    C.transpose_into(w, wt)
 
     # ------------------------------------------------------------------ micro-step bookkeeping
     def _begin_micro(self):

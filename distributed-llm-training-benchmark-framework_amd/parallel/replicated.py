@@ -93,13 +93,10 @@ class ReplicatedEngine(Engine):
             self.rs_out = self.acc = None
         del master_full
         self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
-        self._wt = {}            # (unit index, param index) -> (W view, W^T view of a stacked buffer)
-        self._wt_stack = {}      # (param index, shape) -> [units, K, N] buffer of transposes
-        self._wt_epoch = -1      # optimizer step the cached transposes belong to
         self._ag_pending = {}    # bucket -> async all-gather of updated parameters (deferred step)
         self._defer_opt = (self.stage >= 1 and self.world > 1 and
                            bool(cfg.extra.get("defer_opt", os.environ.get("DLTB_DEFER_OPT", "1") == "1")))
-        self._cache_wt = True    # cached W^T of every matrix for the NT-form dgrad GEMMs
+        self._cache_wt = True    # cached W^T of every matrix for the NT-form dgrad GEMMs (engine.py)
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
         # weight gradients queued and issued as strided-batched GEMMs (parallel/wgrad.py): world 1
@@ -142,47 +139,6 @@ class ReplicatedEngine(Engine):
             self.comm_bytes_per_step = int(per)
 
     # ------------------------------------------------------------------ runtime interface
-    def weight_t(self, unit, i, w):
-        """Cached W^T for the NT-form data-gradient GEMM.  The transposes of one parameter kind
-        live in one stacked buffer, row = reversed unit index (the order of the parameters in the
-        flat buffer), so after an optimizer step all of them are refreshed by ONE batched
-        LDS-tiled transpose launch per kind instead of one launch per block."""
-        if not self._cache_wt or w.dim() != 2 or not w.is_cuda:
-            return None
-        if self._wt_epoch != self.opt_steps:
-            self._refresh_weight_t()
-            self._wt_epoch = self.opt_steps
-        key = (unit.index, i)
-        hit = self._wt.get(key)
-        if hit is not None:
-            return hit[1]
-        g = (i, tuple(w.shape))
-        stack = self._wt_stack.get(g)
-        nunits = len(self.model.units())
-        if stack is None:
-            stack = torch.empty((nunits, w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
-            self._wt_stack[g] = stack
-        wt = stack[nunits - 1 - unit.index]
-        ext().transpose_into(w, wt)          # first use: transpose now
-        self._wt[key] = (w, wt)
-        return wt
-
-    def _refresh_weight_t(self):
-        from .wgrad import strided_batch
-        groups = {}
-        for (uidx, i), (w, wt) in self._wt.items():
-            groups.setdefault((i, tuple(w.shape)), []).append((w, wt))
-        C = ext()
-        for items in groups.values():
-            items.sort(key=lambda it: it[1].data_ptr())
-            W = strided_batch([it[0] for it in items])
-            WT = strided_batch([it[1] for it in items], out=True)
-            if W is not None and WT is not None and len(items) > 1:
-                C.transpose_batched(items[0][0], items[0][1], len(items), W.stride(0), WT.stride(0))
-            else:
-                for w, wt in items:
-                    C.transpose_into(w, wt)
-
     def acquire(self, unit):
         if self._ag_pending:
             b = self._bucket_of.get(id(unit))

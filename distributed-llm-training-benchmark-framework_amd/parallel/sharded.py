@@ -160,6 +160,16 @@ class ShardedEngine(Engine):
             cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
         self._wq = WgradQueue()
         self.wgrad_rows_reversed = self._blocks_reversed()
+        # world 1: every group's gathered view IS its resident shard, so W^T can be cached per
+        # optimizer step like the replicated engines do (NT-form dgrad GEMMs).  Measured
+        # (profiles/cache_weight_t_sharded_r2.txt): TinyGPT-A ZeRO-3 (4 micro-steps per refresh)
+        # 8.04 -> 7.83 ms; FSDP with the reference's one micro-step per optimizer step 8.80 -> 8.93
+        # (the refresh every step costs more than it saves); Mistral-7B ZeRO-3 neutral (GEMMs
+        # -2.4 ms, transposes +1.5 ms per micro-step) for 14.5 GB more HBM.  So: accumulation
+        # windows only, and models below 2B parameters.
+        nparam = sum(u.numel for u in self.model.units())
+        self._cache_wt = (self.world == 1 and self.accum > 1 and nparam < 2_000_000_000
+                          and bool(cfg.extra.get("cache_weight_t", True)))
         if self.world > 1:
             e = self.shard_buf.element_size()
             gathers = 1 if (self.keep_all or not cfg.reshard_after_forward) else 2
@@ -363,6 +373,7 @@ class ShardedEngine(Engine):
             self.comm.all_gather(self.p_flat, mine, async_op=False)
 
     def _after_param_load(self):
+        self._wt_epoch = -1                       # cached transposes are stale
         for grp in self.groups:                   # gathered copies (if any) are stale
             self._release(grp)
         pc = self.p_layout.owner_numel
