@@ -35,6 +35,15 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
     seed = site_seed(seed_ptr, site);
     rk = rng_row_key(seed, (uint32_t)row);
   }
+  uint4 wraw[NV], braw[NV];           // weight / bias issued first: their latency hides under the stats
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int idx = j * 64 + lane;
+    if (idx < nvec) {
+      wraw[j] = ld16<uint4>(w + idx * 8);
+      if (!RMS) braw[j] = ld16<uint4>(b + idx * 8);
+    }
+  }
   float sum = 0.f;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -91,10 +100,10 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
     const int idx = j * 64 + lane;
     if (idx < nvec) {
       float wv[8], o[8];
-      unpack8(ld16<uint4>(w + idx * 8), wv);
+      unpack8(wraw[j], wv);
       if (!RMS) {
         float bv[8];
-        unpack8(ld16<uint4>(b + idx * 8), bv);
+        unpack8(braw[j], bv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (v[j][e] - mean) * rstd * wv[e] + bv[e];
       } else {
@@ -204,6 +213,14 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
     const float rstd = rstd_in[row];
     float g[NV][8], xh[NV][8];
     float s1 = 0.f, s2 = 0.f;
+    uint4 rraw[NV];                                      // residual gradient: issued with dy / s, so its
+    if (HAS_RES_GRAD) {                                  // latency hides under the row reductions
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < nvec) rraw[j] = ld16<uint4>(dres + base + idx * 8);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int idx = j * 64 + lane;
@@ -233,7 +250,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
         for (int e = 0; e < 8; ++e) o[e] = rstd * (g[j][e] - s1 - xh[j][e] * s2);
         if (HAS_RES_GRAD) {
           float rv[8];
-          unpack8(ld16<uint4>(dres + base + idx * 8), rv);
+          unpack8(rraw[j], rv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] += rv[e];
         }
