@@ -445,8 +445,13 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs P) {
 // so each probability costs bfe + 2 and + sub + mul besides its exp.
 template <int D>
 constexpr int dkdv_ks() { return D == 64 ? 2 : 1; }
+// dropout words in LDS: [4 subs][kTile rows] with a 4-word pad per sub, so the two subs a wave
+// reads together (lanes with key bit 2 clear / set) and the 4 subs one store instruction writes
+// start 68 words apart -- different banks, where an unpadded 64-word stride put them all on the
+// same bank (the 12 % LDS bank conflicts of profiles/attention_pmc_tinygpt_a.txt)
+constexpr int kMaskStride = kTile + 4;
 template <int D>
-constexpr int dkdv_stage_bytes() { return 2 * kTile * D * 2 + 2 * kTile * 4 + kTile * 16; }
+constexpr int dkdv_stage_bytes() { return 2 * kTile * D * 2 + 2 * kTile * 4 + 4 * kMaskStride * 4; }
 template <int D>
 constexpr int dkdv_smem_bytes() {
   constexpr int a = 2 * dkdv_ks<D>() * dkdv_stage_bytes<D>();
@@ -549,7 +554,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     }
     if (DROP) {   // [sub][row]: a lane's 4 consecutive query rows are one ds_read_b128
       const int row = stid >> 2, sb = stid & 3;
-      reinterpret_cast<uint32_t*>(f + 2 * kTile)[sb * kTile + row] = mword;
+      reinterpret_cast<uint32_t*>(f + 2 * kTile)[sb * kMaskStride + row] = mword;
     }
   };
   load(0);
@@ -607,7 +612,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
         uint4 M4;
         if (DROP) {
           Dl = *reinterpret_cast<const float4*>(dlt + ql);
-          M4 = *reinterpret_cast<const uint4*>(mws + msub * kTile + ql);
+          M4 = *reinterpret_cast<const uint4*>(mws + msub * kMaskStride + ql);
         }
         const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
         const uint32_t Mv[4] = {M4.x, M4.y, M4.z, M4.w};
