@@ -45,6 +45,7 @@
 #define DLTB_ATTN_PIPE 0
 #endif
 
+#include "attn_mask.h"
 #include "common.h"
 #include "mfma_tiles.h"
 
@@ -139,30 +140,12 @@ DLTB_DEV void store_acc_rows_f32(float* dst_row, const f32x16* acc, float scale,
 }
 
 // =============================================================================== dropout mask
-// word (bh, t, h, q) at ((bh*nT + t)*2 + h)*T + q; bit 16n + i <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h
+// (layout and body: attn_mask.h)
+static_assert(kTile == kMaskKeyTile, "the packed mask tiles keys like the attention kernels");
 __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ mask, int T, uint32_t thr16,
                                                         const int64_t* __restrict__ seed_ptr, int64_t site) {
   // grid: x = query chunks of 256, y = (bh * nT + t) * 2 + h  (32-bit index math only)
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= T) return;
-  const int nT = T / kTile;
-  const uint32_t g = blockIdx.y;
-  const int h = g & 1;
-  const int t = (g >> 1) % nT;
-  const uint32_t bh = (g >> 1) / nT;
-  const uint64_t seed = site_seed(seed_ptr, site);
-  const uint32_t rk = rng_row_key(seed, bh * (uint32_t)T + q);
-  uint32_t bits = 0;
-#pragma unroll
-  for (int n = 0; n < 2; ++n)
-#pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      const uint32_t key = (uint32_t)(t * kTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
-      const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
-      bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << (16 * n + i);
-      bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << (16 * n + i + 1);
-    }
-  mask[(size_t)g * T + q] = bits;
+  attn_mask_word(mask, T, thr16, seed_ptr, site, blockIdx.x * 256 + threadIdx.x, blockIdx.y);
 }
 
 // =============================================================================== forward

@@ -9,6 +9,7 @@
 // per-column dgamma/dbeta partials; a block folds its 4 waves through LDS float atomics and
 // writes one fp32 partial row; `norm_colreduce` sums the partials into the bf16 gradient slot
 // (overwrite or accumulate).  Reference ops: nn.LayerNorm (train_harness.py:112,117,56).
+#include "attn_mask.h"
 #include "common.h"
 
 namespace {
@@ -16,14 +17,13 @@ namespace {
 constexpr int kRowsPerWave = 4;   // backward: rows per wave
 constexpr int kWaves = 4;
 
+// one wave = one row (the body of norm_fwd_kernel and of norm_fwd_mask_kernel's norm blocks)
 template <int NV, bool RMS, bool HAS_RES>
-__global__ __launch_bounds__(256) void norm_fwd_kernel(
+DLTB_DEV void norm_fwd_row(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ b, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int d, float eps,
-    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site) {
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site, int row, int lane) {
   if (row >= N) return;
   const int nvec = d >> 3;
   const size_t base = (size_t)row * d;
@@ -112,6 +112,47 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
       }
       *reinterpret_cast<uint4*>(y + base + idx * 8) = pack8(o);
     }
+  }
+}
+
+template <int NV, bool RMS, bool HAS_RES>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ b, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int d, float eps,
+    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site) {
+  norm_fwd_row<NV, RMS, HAS_RES>(x, r, w, b, s_out, y, mean_out, rstd_out, N, d, eps, thr16, drop_scale,
+                                 seed_ptr, site, blockIdx.x * kWaves + (threadIdx.x >> 6), threadIdx.x & 63);
+}
+
+// A block's first LayerNorm and its attention-dropout mask in ONE launch (horizontal fusion):
+// blocks [0, nb_norm) are norm_fwd_kernel's blocks, the rest attn_mask_kernel's (flattened
+// (query chunk, tile group) grid).  The mask hash is VALU-bound and the row norm waits on memory,
+// so the two kinds of waves share the CUs instead of running back to back.
+struct MaskJob {
+  uint32_t* mask;
+  int T;
+  uint32_t thr16;
+  const int64_t* seed;
+  int64_t site;
+  int gx;              // query chunks of 256 per tile group
+};
+
+template <int NV, bool RMS, bool HAS_RES>
+__global__ __launch_bounds__(256) void norm_fwd_mask_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ b, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int d, float eps,
+    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site, int nb_norm,
+    MaskJob mj) {
+  const int bid = blockIdx.x;
+  if (bid < nb_norm) {
+    norm_fwd_row<NV, RMS, HAS_RES>(x, r, w, b, s_out, y, mean_out, rstd_out, N, d, eps, thr16, drop_scale,
+                                   seed_ptr, site, bid * kWaves + (threadIdx.x >> 6), threadIdx.x & 63);
+  } else {
+    const int m = bid - nb_norm;
+    attn_mask_word(mj.mask, mj.T, mj.thr16, mj.seed, mj.site, (m % mj.gx) * 256 + threadIdx.x,
+                   (uint32_t)(m / mj.gx));
   }
 }
 
@@ -428,6 +469,49 @@ void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, v
   } else {
     if (r) launch_fwd_t<false, true>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site);
     else   launch_fwd_t<false, false>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site);
+  }
+}
+
+template <bool RMS, bool HAS_RES>
+void launch_fwd_mask_t(int nv, int nb_norm, int nb_mask, hipStream_t st, const bf16_t* x, const bf16_t* r,
+                       const bf16_t* w, const bf16_t* b, bf16_t* s_out, bf16_t* y, float* mean, float* rstd,
+                       int N, int d, float eps, uint32_t thr, float scale, const int64_t* seed, int64_t site,
+                       const MaskJob& mj) {
+  const dim3 grid(nb_norm + nb_mask);
+#define DLTB_NFM(NVV)                                                                                 \
+  hipLaunchKernelGGL((norm_fwd_mask_kernel<NVV, RMS, HAS_RES>), grid, dim3(256), 0, st, x, r, w, b,   \
+                     s_out, y, mean, rstd, N, d, eps, thr, scale, seed, site, nb_norm, mj)
+  switch (nv) {
+    case 1: DLTB_NFM(1); break;
+    case 2: DLTB_NFM(2); break;
+    case 3: DLTB_NFM(3); break;
+    case 4: DLTB_NFM(4); break;
+    case 6: DLTB_NFM(6); break;
+    default: DLTB_NFM(8); break;
+  }
+#undef DLTB_NFM
+}
+
+void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void* b, void* s_out, void* y,
+                        float* mean, float* rstd, int N, int d, float eps, bool rms, uint32_t thr16,
+                        float drop_scale, const int64_t* seed, int64_t site, uint32_t* mask, int B, int T,
+                        int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st) {
+  const int nv = nv_for(d);
+  const MaskJob mj{mask, T, mask_thr16, mask_seed, mask_site, cdiv(T, 256)};
+  const int nb_norm = cdiv(N, kWaves);
+  const int nb_mask = mj.gx * B * Hq * (T / kMaskKeyTile) * 2;
+  auto X = (const bf16_t*)x;
+  auto R = (const bf16_t*)r;
+  auto W = (const bf16_t*)w;
+  auto Bi = (const bf16_t*)b;
+  auto S = (bf16_t*)s_out;
+  auto Y = (bf16_t*)y;
+  if (rms) {
+    if (r) launch_fwd_mask_t<true, true>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
+    else   launch_fwd_mask_t<true, false>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
+  } else {
+    if (r) launch_fwd_mask_t<false, true>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
+    else   launch_fwd_mask_t<false, false>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
   }
 }
 

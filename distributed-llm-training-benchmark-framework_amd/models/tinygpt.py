@@ -114,13 +114,13 @@ class _BlockFn(torch.autograd.Function):
         H, d = cfg.n_head, cfg.n_embd
         p = model.drop_p
         lb = model.layer_buffer(i)          # layer-strided GEMM operands (batched weight gradients)
-        amask = F_.attn_mask(B, T, H, p, rt.seed, model.site_attn(i), x_in)
-        if m_in is None:                    # block 0: the embedding output
+        # LN1 (with the previous block's MLP dropout + residual) and this block's attention-dropout
+        # mask: one launch on the GPU
+        x, h1, mean1, rstd1, amask = F_.norm_fwd_mask(
+            x_in, m_in, ln1w, ln1b, LN_EPS, False, p if m_in is not None else 0.0, rt.seed,
+            model.site_mlp(i - 1) if m_in is not None else 0, lb and lb.h1, B, T, H, p, model.site_attn(i))
+        if m_in is None:                    # block 0: the embedding output is the residual stream
             x = x_in
-            _, h1, mean1, rstd1 = F_.norm_fwd(x, None, ln1w, ln1b, LN_EPS, False, y_out=lb and lb.h1)
-        else:                               # x = x1' + Dropout(m') of the previous block, fused
-            x, h1, mean1, rstd1 = F_.norm_fwd(x_in, m_in, ln1w, ln1b, LN_EPS, False, p, rt.seed,
-                                              model.site_mlp(i - 1), y_out=lb and lb.h1)
         qkv = F_.linear_fwd(h1, win, bin_)
         o, lse, amask = F_.attn_fwd(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], B, T, H, H,
                                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i),

@@ -40,6 +40,18 @@ def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0, y_out=None):
     return s, _into(y_out, y), mean, rstd
 
 
+def norm_fwd_mask(x, r, w, b, eps, rms, p, seed, site, y_out, B, T, Hq, p_attn, attn_site):
+    """norm_fwd plus the attention-dropout mask of (B, T, Hq) at ``attn_site``, on the GPU in one
+    launch (csrc/norm.hip norm_fwd_mask_kernel).  Returns (s, y, mean, rstd, mask); mask is None on
+    the CPU or without attention dropout."""
+    if _gpu(x) and p_attn > 0:
+        s_, y, mean, rstd, mask = ext().norm_fwd_mask(x, r, w, b, eps, rms, p, seed.device_tensor, site, y_out,
+                                                      B, T, Hq, p_attn, attn_site)
+        return (s_ if r is not None else None), y, (None if rms else mean), rstd, mask
+    s_, y, mean, rstd = norm_fwd(x, r, w, b, eps, rms, p, seed, site, y_out)
+    return s_, y, mean, rstd, attn_mask(B, T, Hq, p_attn, seed, attn_site, x)
+
+
 # colpart segment kinds (csrc/colreduce.hip)
 _PLAIN, _GELU, _DROP, _LN, _RMS = 0, 1, 2, 3, 4
 

@@ -477,3 +477,22 @@ def test_transpose_batched():
     C.transpose_batched(src[0], dst[0], nb, R * Cc + gap, Cc * R)
     for i in range(nb):
         assert torch.equal(dst[i], src[i].t()), i
+
+
+@pytest.mark.parametrize("with_res", [False, True])
+def test_norm_fwd_mask_fused_matches_separate(with_res):
+    """norm_fwd_mask (one launch: LN rows + attention-dropout mask blocks) is bitwise the separate
+    norm_fwd and attn_mask launches."""
+    C = ext()
+    B, T, H, d = 1, 512, 8, 1024
+    x, w, b = rnd(B * T, d), rnd(d, scale=0.1) + 1, rnd(d, scale=0.1)
+    r = rnd(B * T, d) if with_res else None
+    sd = seed_obj(77)
+    p = 0.1 if with_res else 0.0
+    s0, y0, m0, rs0 = C.norm_fwd(x, r, w, b, 1e-5, False, p, sd.device_tensor if p else None, 4, None)
+    mk0 = C.attn_mask(B, T, H, 0.1, sd.device_tensor, 9, x)
+    s1, y1, m1, rs1, mk1 = C.norm_fwd_mask(x, r, w, b, 1e-5, False, p, sd.device_tensor, 4, None, B, T, H, 0.1, 9)
+    assert torch.equal(y0, y1) and torch.equal(m0, m1) and torch.equal(rs0, rs1)
+    if with_res:
+        assert torch.equal(s0, s1)
+    assert torch.equal(mk0, mk1)
