@@ -196,3 +196,26 @@ def test_world2_deferred_optimizer_step_is_exact():
         res = torch.load(out, weights_only=True)
     for n in res["1"]:
         assert torch.equal(res["1"][n], res["0"][n]), n
+
+
+def test_zero3_288gb_config_keeps_gathered_params():
+    """configs/deepspeed/zero3_mi355x_288gb.json: a Mistral-7B-sized model fits under
+    stage3_max_live_parameters, so the ZeRO-3 engine keeps gathered parameters resident
+    (keep_all); the reference's zero3.json (1e9) does not for that size."""
+    import json
+    import os
+    from dltb.parallel.strategy import load_deepspeed_config
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    big = load_deepspeed_config(os.path.join(root, "configs", "deepspeed", "zero3_mi355x_288gb.json"))
+    ref = load_deepspeed_config(os.path.join(root, "configs", "deepspeed", "zero3.json"))
+    m7b = 7_241_732_096
+    for cfg, keep in ((big, True), (ref, False)):
+        z = cfg["zero_optimization"]
+        assert (m7b <= z["stage3_max_live_parameters"] and m7b <= z["stage3_max_reuse_distance"]) == keep
+    assert {k: v for k, v in big.items() if k != "_comment" and k != "zero_optimization"} == \
+        {k: v for k, v in ref.items() if k != "_comment" and k != "zero_optimization"}
+    torch.manual_seed(0)
+    m = TinyGPT(get_model_config("tiny", 16, dropout=0.0))
+    e = make_engine(m, engine_config("zero3", 2, "reference", ds_config=big), "cpu")
+    assert e.keep_all
+    json.dumps(big)
