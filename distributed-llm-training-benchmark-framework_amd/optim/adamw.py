@@ -77,7 +77,15 @@ class FlatAdamW:
         b1, b2 = self.betas
         bc1 = 1.0 - b1 ** self.step_count
         bc2 = 1.0 - b2 ** self.step_count
-        self.hp.copy_(torch.tensor([self._lr_now, self._lr_now / bc1, 1.0 / math.sqrt(bc2), 0.0]))
+        vals = (self._lr_now, self._lr_now / bc1, 1.0 / math.sqrt(bc2), 0.0)
+        if self.hp.is_cuda:
+            # one fill per value: the scalars travel as kernel arguments.  A copy_ from a (pageable)
+            # host tensor would synchronize the stream -- a full pipeline drain at every window
+            # boundary of an eager (multi-rank) run
+            for i, v in enumerate(vals):
+                self.hp[i:i + 1].fill_(v)
+        else:
+            self.hp.copy_(torch.tensor(vals))
 
     def launch(self, grad: torch.Tensor, gscale: torch.Tensor = None):
         b1, b2 = self.betas

@@ -52,6 +52,17 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / a.steps
     print(f"host enqueue {host * 1e3:.3f} ms/step, wall {wall * 1e3:.3f} ms/step")
+    # the pure host cost: enqueue 2 steps behind a long GPU sleep, so the queue never makes the
+    # host wait (with a shallow backlog "enqueue" above is bounded by the GPU itself)
+    for _ in range(3):
+        torch.cuda.synchronize()
+        torch.cuda._sleep(int(2.4e8))          # ~100 ms of GPU cycles ahead of the steps
+        t0 = time.perf_counter()
+        for _ in range(2):
+            step()
+        h2 = (time.perf_counter() - t0) / 2
+        torch.cuda.synchronize()
+        print(f"host-only cost (GPU busy ahead): {h2 * 1e3:.3f} ms/step")
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(a.steps):
