@@ -153,7 +153,7 @@ std::vector<BltResult> dltb_blaslt_sweep(const BltProblem& p, const void* A, con
                    hipblaslt_ext::getSolutionNameFromAlgo(handle(), algos[i].algo)});
   }
   std::sort(base.begin(), base.end());
-  if ((int)base.size() > refine) base.resize(refine);
+  if (refine > 0 && (int)base.size() > refine) base.resize(refine);   // refine <= 0: every solution
   for (auto& b : base) {
     auto& a = algos[b.second];
     for (int sk : splitks)

@@ -31,7 +31,8 @@ struct BltResult {
   std::string name;
 };
 
-// Time all solutions (default tuning), then the fastest `refine` of them under every
+// Time all solutions (default tuning), then the fastest `refine` of them (all of them when
+// refine <= 0: a large-tile solution is slow alone but can win with split-K) under every
 // (splitK, wgm) pair.  A, B, C must be device buffers of the problem's extents; C is overwritten.
 std::vector<BltResult> dltb_blaslt_sweep(const BltProblem& p, const void* A, const void* B, void* C,
                                          const void* bias, int iters, const std::vector<int>& splitks,
