@@ -217,8 +217,12 @@ class Engine(ParamRuntime):
             return hit[1]
         g = (i, tuple(w.shape))
         stack = self._wt_stack.get(g)
-        # one row per unit holding a parameter of this kind, in reversed unit order
-        rows = [u.index for u in reversed(self.model.units()) if len(u.shapes) > i and u.shapes[i] == g[1]]
+        # one row per unit holding a parameter of this kind, in the order of the parameters in the
+        # engine's flat buffers (reversed unit order unless the engine says otherwise), so the
+        # refresh finds W and W^T equally spaced and batches them
+        units = self.model.units()
+        order = reversed(units) if getattr(self, "wgrad_rows_reversed", True) else units
+        rows = [u.index for u in order if len(u.shapes) > i and u.shapes[i] == g[1]]
         if stack is None:
             stack = torch.empty((len(rows), w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
             self._wt_stack[g] = stack

@@ -164,7 +164,8 @@ class ShardedEngine(Engine):
         # optimizer step like the replicated engines do (NT-form dgrad GEMMs).  Measured
         # (profiles/cache_weight_t_sharded_r2.txt): TinyGPT-A ZeRO-3 (4 micro-steps per refresh)
         # 8.04 -> 7.83 ms; FSDP with the reference's one micro-step per optimizer step 8.80 -> 8.93
-        # (the refresh every step costs more than it saves); Mistral-7B ZeRO-3 neutral (GEMMs
+        # (the refresh every step costs more than it saves; 8.66 vs 8.68 once the refresh is batched,
+        # profiles/cache_weight_t_sharded_r2.txt); Mistral-7B ZeRO-3 neutral (GEMMs
         # -2.4 ms, transposes +1.5 ms per micro-step) for 14.5 GB more HBM.  So: accumulation
         # windows only, and models below 2B parameters.
         nparam = sum(u.numel for u in self.model.units())
