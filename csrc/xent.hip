@@ -16,7 +16,7 @@ __global__ __launch_bounds__(512) void xent_kernel(bf16_t* __restrict__ logits,
                                                   const int64_t* __restrict__ targets,
                                                   float* __restrict__ loss, int V,
                                                   int64_t ignore_index) {
-  __shared__ float red[8];
+  __shared__ float red[8], red2[8];
   __shared__ float s_tlogit;
   const int row = blockIdx.x;
   bf16_t* z = logits + (long)row * V;
@@ -24,45 +24,66 @@ __global__ __launch_bounds__(512) void xent_kernel(bf16_t* __restrict__ logits,
   const bool valid = (t != ignore_index) && t >= 0 && t < V;
   if (threadIdx.x == 0) s_tlogit = valid ? bf2f(z[t]) : 0.f;
   const int nvec = V >> 3;
-  uint4 v[VPT];
-  float m = -INFINITY;
+  // one pass over the row: per-thread max m_t and e = exp(z - m_t) kept in registers, then ONE
+  // block reduction of (m_t, sum e) pairs (online-softmax merge); the output rescales e by
+  // exp(m_t - m) / sum instead of recomputing the exponentials
+  float e[VPT][8];
+  float mt = -INFINITY;
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int i = j * 512 + threadIdx.x;
     if (i < nvec) {
-      v[j] = ld16<uint4>(z + i * 8);
-      float f[8];
-      unpack8(v[j], f);
+      unpack8(ld16<uint4>(z + i * 8), e[j]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) m = fmaxf(m, f[e]);
+      for (int k = 0; k < 8; ++k) mt = fmaxf(mt, e[j][k]);
     }
   }
-  m = block_max(m, red);
-  float s = 0.f;
+  float st = 0.f;
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int i = j * 512 + threadIdx.x;
     if (i < nvec) {
-      float f[8];
-      unpack8(v[j], f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) s += __expf(f[e] - m);
+      for (int k = 0; k < 8; ++k) {
+        e[j][k] = __expf(e[j][k] - mt);
+        st += e[j][k];
+      }
     }
   }
-  s = block_sum(s, red);
-  const float inv = 1.f / s;
-  if (threadIdx.x == 0) loss[row] = valid ? (m + __logf(s) - s_tlogit) : 0.f;
+  // (m, s) pairs: wave butterfly, then the 8 waves through LDS (fixed order)
+  float m = mt, sm = st;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float mo = __shfl_xor(m, off);
+    const float so = __shfl_xor(sm, off);
+    const float mn = fmaxf(m, mo);
+    sm = (m == -INFINITY ? 0.f : sm * __expf(m - mn)) + (mo == -INFINITY ? 0.f : so * __expf(mo - mn));
+    m = mn;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[wid] = m;
+    red2[wid] = sm;
+  }
+  __syncthreads();
+  float M = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) M = fmaxf(M, red[w]);
+  float S = 0.f;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) S += red[w] == -INFINITY ? 0.f : red2[w] * __expf(red[w] - M);
+  if (threadIdx.x == 0) loss[row] = valid ? (M + __logf(S) - s_tlogit) : 0.f;
+  const float scale = mt == -INFINITY ? 0.f : __expf(mt - M) / S;
 #pragma unroll
   for (int j = 0; j < VPT; ++j) {
     const int i = j * 512 + threadIdx.x;
     if (i < nvec) {
       float f[8];
-      unpack8(v[j], f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float p = valid ? __expf(f[e] - m) * inv : 0.f;
-        if (valid && i * 8 + e == t) p -= 1.f;
-        f[e] = p;
+      for (int k = 0; k < 8; ++k) {
+        float p = valid ? e[j][k] * scale : 0.f;
+        if (valid && i * 8 + k == t) p -= 1.f;
+        f[k] = p;
       }
       *reinterpret_cast<uint4*>(z + i * 8) = pack8(f);
     }
