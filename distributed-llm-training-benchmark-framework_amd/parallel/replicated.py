@@ -54,9 +54,27 @@ class ReplicatedEngine(Engine):
         ds_cap = cfg.extra.get("reduce_bucket_elems")
         if ds_cap:
             bucket_elems = min(bucket_elems, int(ds_cap)) if bucket_elems else int(ds_cap)
+        # weight gradients queued and issued as strided-batched GEMMs (parallel/wgrad.py): world 1
+        # flushes once per backward, world > 1 per bucket right before its collective
+        self.defer_wgrad = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
+        # World > 1: a bucket's dW products are one batched GEMM per kind, so the bucket's block count
+        # is the batch size.  hipBLASLt's batched kernels run 4 or 8 TinyGPT-A blocks at 52-58 us per
+        # block but 2-3 blocks at 75-80 and 6 at 68 (profiles/wgrad_batch_size_r2.txt): buckets are
+        # rounded up to a multiple of 4 of the model's repeated unit (64 MiB -> 4 blocks, 101 MB).
+        # Only the embedding (the unit that finishes last) then keeps a bucket of its own: a solo block 0
+        # would be a 1-block batch (110 us) and leave 3 blocks for the group before it.
+        mult = int(cfg.extra.get("bucket_unit_multiple", 4))
+        solo_tail = 2
+        if self.world > 1 and self.defer_wgrad and bucket_elems > 0 and mult > 1:
+            sizes = sorted(u.numel for u in units)
+            grp = mult * sizes[len(sizes) // 2]          # the repeated unit: a transformer block
+            bucket_elems = -(-bucket_elems // grp) * grp
+            if ds_cap:
+                bucket_elems = min(bucket_elems, max(int(ds_cap), grp))
+            solo_tail = 1
         shard = self.stage >= 1
         self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
-                                      solo_tail=int(cfg.extra.get("solo_tail_units", 2)))
+                                      solo_tail=int(cfg.extra.get("solo_tail_units", solo_tail)))
         dev, dt = self.device, self.compute_dtype
         master_full = torch.zeros(L.total, dtype=torch.float32, device=dev)
         for s in L.slots.values():
@@ -99,9 +117,6 @@ class ReplicatedEngine(Engine):
         self._cache_wt = True    # cached W^T of every matrix for the NT-form dgrad GEMMs (engine.py)
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
-        # weight gradients queued and issued as strided-batched GEMMs (parallel/wgrad.py): world 1
-        # flushes once per backward, world > 1 per bucket right before its collective
-        self.defer_wgrad = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
         self._wq = WgradQueue()
         # Window-wide weight gradients: where no collective reads a gradient before the window ends
         # (world 1, or the window-reduced ZeRO-1 / DDP paths), the model keeps every micro-step's
