@@ -504,7 +504,16 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const int wv = __builtin_amdgcn_readfirstlane(kw);
   float vl = 0.f, vd = 0.f;
   uint32_t mword = 0;
-  auto tile_of = [&](int j, int& g, int& t) { g = g0 + j / nit; t = t_begin + (j % nit) * KS + sp; };
+  const int spu = __builtin_amdgcn_readfirstlane(sp);   // wave-uniform: tile math stays in SGPRs
+  auto tile_of = [&](int j, int& g, int& t) { g = g0 + j / nit; t = t_begin + (j % nit) * KS + spu; };
+  // loop-invariant per-lane parts of every streamed address (the Q / dO LDS-DMA offsets, the
+  // dropout-word offset); per tile only wave-uniform (SGPR) bases change -- no per-tile VALU
+  // address arithmetic (64-bit multiplies) in the loop
+  uint32_t qoff[GldsTile<D, kTile>::NI], doff[GldsTile<D, kTile>::NI];
+  GldsTile<D, kTile>::offsets(P.q_stride, wv, lane, qoff);
+  GldsTile<D, kTile>::offsets(P.do_stride, wv, lane, doff);
+  const int mrow = stid >> 2, msb = stid & 3;
+  const uint32_t moff = (uint32_t)(msb * T + mrow);    // ((.. + (sb >> 1)) * 2 + (sb & 1)) * T + row
   auto load = [&](int j) {
     int g, t;
     tile_of(j, g, t);
@@ -514,16 +523,15 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     // Q / dO tiles straight into the stage buffer by LDS-DMA (it is not being read: the previous
     // reader of this buffer finished before the last barrier)
     char* base = smem + ((j & 1) * KS + sp) * SB;
-    GldsTile<D, kTile>::load(P.q + (long)b * T * P.q_stride + hq * D, P.q_stride, t * kTile, base, wv, lane);
-    GldsTile<D, kTile>::load(P.dout + (long)b * T * P.do_stride + hq * D, P.do_stride, t * kTile, base + TB, wv, lane);
+    const long r0 = (long)b * T + t * kTile;
+    GldsTile<D, kTile>::load_sv(P.q + r0 * P.q_stride + hq * D, qoff, base, wv);
+    GldsTile<D, kTile>::load_sv(P.dout + r0 * P.do_stride + hq * D, doff, base + TB, wv);
     if (stid < kTile) {   // row constants, loaded straight into the S / dP accumulators
-      vl = -P.lse[bq * T + t * kTile + stid] * inv_scale;
-      vd = -P.delta[bq * T + t * kTile + stid] * inv_s;
+      const long rc = bq * T + t * kTile;
+      vl = -P.lse[rc + stid] * inv_scale;
+      vd = -P.delta[rc + stid] * inv_s;
     }
-    if (DROP) {
-      const int row = stid >> 2, sb = stid & 3;
-      mword = P.mask[((bq * nT + (kb * 2 + (sb >> 1))) * 2 + (sb & 1)) * T + t * kTile + row];
-    }
+    if (DROP) mword = P.mask[((bq * nT + kb * 2) * 2) * T + t * kTile + moff];
   };
   auto store = [&](int j) {
     int g, t;
@@ -535,10 +543,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
       f[stid] = vl;
       f[kTile + stid] = vd;
     }
-    if (DROP) {   // [sub][row]: a lane's 4 consecutive query rows are one ds_read_b128
-      const int row = stid >> 2, sb = stid & 3;
-      reinterpret_cast<uint32_t*>(f + 2 * kTile)[sb * kMaskStride + row] = mword;
-    }
+    if (DROP)     // [sub][row]: a lane's 4 consecutive query rows are one ds_read_b128
+      reinterpret_cast<uint32_t*>(f + 2 * kTile)[msb * kMaskStride + mrow] = mword;
   };
   load(0);
   store(0);
