@@ -27,22 +27,31 @@
 // mapping: word (bh, t, h, q) holds, in bit 16n + i, the decision for key 64t + 32n + (i&3) +
 // 8(i>>2) + 4h of query q — so forward and dQ lanes read one coalesced word per 64-key tile and the
 // dK/dV kernel stages 4 words per query row in LDS.  The hash runs 1x instead of 3x, and the
-// softmax kernels pay 2 VALU ops per probability for dropout.
+// softmax kernels pay for dropout 1.5 VALU ops per probability in the forward (on the packed bf16
+// P pairs, attn_mask.h) and 2 in the backward.  The softmax scale c = scale * log2(e) is folded into
+// the operand each wave holds in registers (Q in the forward and dQ, K in dK/dV) and the row
+// constants (-m, -lse log2 e, -delta/s) are the S / dP chains' initial accumulators, so the score
+// tiles come out of the MFMAs as exp2 arguments.
 #include <cstdlib>
 
-// DLTB_ATTN_PK=1: the softmax math as packed fp32 (v_pk_fma / v_pk_mul / v_pk_add, two scores per
-// instruction).  Default 0: scalar f32 ops, and the file is built with -fno-slp-vectorize so the
-// compiler does not re-pack them: beside MFMAs a packed f32 op costs far more issue time than the
-// two scalar ops it replaces (MI355X_MICROARCH 'price of one filler beside MFMAs').
-#ifndef DLTB_ATTN_PK
-#define DLTB_ATTN_PK 0
-#endif
+// Softmax math is scalar f32: the file is built with -fno-slp-vectorize so the compiler does not
+// pack it into v_pk_* ops, which beside MFMAs cost more issue time than the two scalar ops they
+// replace (MI355X_MICROARCH 'price of one filler beside MFMAs'; measured 1-3 % slower,
+// profiles/attention_ab_r2.txt).
 // DLTB_ATTN_PIPE=1: the backward kernels compute S / dP of BOTH 32-row sub-tiles of a
 // 64-row tile before the first softmax, so one sub-tile's MFMAs run under the other's VALU softmax
 // inside the same wave.  Default 0 (sub-tile after sub-tile): measured equal or faster on MI355X
 // (TinyGPT-A dK/dV 56.2-57.2 vs 58.5-59.0 us, profiles/attention_ab_r2.txt).
 #ifndef DLTB_ATTN_PIPE
 #define DLTB_ATTN_PIPE 0
+#endif
+
+// key splits per workgroup at D = 64 (A/B builds: csrc/build.py --tag T -D DLTB_FWD_KS64=2)
+#ifndef DLTB_FWD_KS64
+#define DLTB_FWD_KS64 3
+#endif
+#ifndef DLTB_DQ_KS64
+#define DLTB_DQ_KS64 3
 #endif
 
 #include "attn_mask.h"
@@ -155,7 +164,7 @@ __global__ __launch_bounds__(256) void attn_mask_kernel(uint32_t* __restrict__ m
 // Online softmax with a lazy rescale: the running max m only moves (and O, l are rescaled) when a
 // tile's row max exceeds m by more than kRescaleLog2 (p <= 2^8, safe in f32 and bf16); the decision
 // is wave-uniform so the rescale is a branch, not per-tile work.  The causal mask is applied on
-// diagonal tiles only.  Dropout: p & sbfe(keep_word, bit) (2 VALU per probability).
+// diagonal tiles only.  Dropout: on the packed bf16 pairs (pack_frag_keep).
 constexpr float kRescaleLog2 = 8.f;
 
 template <int I>
@@ -183,12 +192,54 @@ DLTB_DEV bfx8 pack_frag(const f32x16& x, int s) {      // regs 8s .. 8s+7 -> bf1
   return f;
 }
 
+// pack_frag of sub-tile N's registers 8 S .. 8 S + 7 with the dropout applied to the PACKED pairs:
+// pair j = 8N + 4S + k has its keep bits at 15 - j / 31 - j (attn_mask.h mask_bit), so (mw << j)
+// holds them as the sign bits of its two halves and v_perm_b32 selector 8 / 9 replicates each into
+// its 16-bit half: shift + perm + and per two probabilities.
+template <int N, int S, bool DROP>
+DLTB_DEV bfx8 pack_frag_keep(const f32x16& x, uint32_t mw) {
+  typedef h16_t bfx2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  uint4 w;
+  uint32_t* wp = reinterpret_cast<uint32_t*>(&w);
+  static_for<4>([&](auto K) {
+    constexpr int k = K;
+    const f32x2 p = {x[8 * S + 2 * k], x[8 * S + 2 * k + 1]};
+    uint32_t d = __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bfx2));
+    if constexpr (DROP) {
+      constexpr int j = 8 * N + 4 * S + k;
+      static_assert(mask_bit(N, 8 * S + 2 * k) == 15 - j && mask_bit(N, 8 * S + 2 * k + 1) == 31 - j,
+                    "packed keep-bit layout");
+      const uint32_t sh = mw << j;
+      d &= __builtin_amdgcn_perm(sh, sh, 0x09090808u);
+    }
+    wp[k] = d;
+  });
+  return __builtin_bit_cast(bfx8, w);
+}
+
+// an 8-element fragment times c, rounded back to the operand format (the softmax scale folded
+// into the operand held in registers: one multiply per element per wave instead of one per score)
+DLTB_DEV bfx8 scale_frag(bfx8 f, float c) {
+  typedef float f32x8 __attribute__((ext_vector_type(8)));
+  return __builtin_convertvector(__builtin_convertvector(f, f32x8) * c, bfx8);
+}
+
+// keep ? x : y for keep bit BIT of mw: a v_bfe_i32 mask, then a bitwise select the compiler emits
+// as one v_bfi_b32 / v_bitop3_b32.  Only the bfe is inline asm: x is an MFMA result, and hipcc does
+// not insert the MFMA -> VALU read wait states in front of an inline-asm reader.
 template <int BIT>
-DLTB_DEV float keep_and(float p, uint32_t mw) {
-  // sign-extended 1-bit field -> 0 / ~0 mask; asm keeps the compiler from re-forming and+cmp+cndmask
+DLTB_DEV float keep_sel(float x, float y, uint32_t mw) {
   uint32_t k;
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(mw), "n"(BIT));
-  return __uint_as_float(__float_as_uint(p) & k);
+  return __uint_as_float((k & __float_as_uint(x)) | (~k & __float_as_uint(y)));
+}
+
+DLTB_DEV f32x16 splat16(float v) {
+  f32x16 r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r[i] = v;
+  return r;
 }
 
 // XCD-aware block order: consecutive workgroup ids land on different XCDs (round robin over 8),
@@ -205,7 +256,7 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
 }
 
 template <int D>
-constexpr int fwd_ks() { return D == 64 ? 3 : 2; }   // KS = 4 (2-deep ring, 128 VGPRs) measured 2 % faster: not worth the spill risk
+constexpr int fwd_ks() { return D == 64 ? DLTB_FWD_KS64 : 2; }   // KS = 4 (2-deep ring, 128 VGPRs) measured 2 % faster: not worth the spill risk
 template <int D, int KS>
 constexpr int fwd_nst() { return D == 64 && KS < 4 ? 3 : 2; }  // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
 template <int D>
@@ -232,7 +283,8 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   {
     const bf16_t* qrow = P.q + ((long)b * T + qi) * P.q_stride + hq * D;
 #pragma unroll
-    for (int s = 0; s < D / 16; ++s) qf[s] = __builtin_bit_cast(bfx8, ld16<uint4>(qrow + 16 * s + 8 * h));
+    for (int s = 0; s < D / 16; ++s)       // Q c: S' = (Q c) K^T is already in log2 units
+      qf[s] = scale_frag(__builtin_bit_cast(bfx8, ld16<uint4>(qrow + 16 * s + 8 * h)), P.scale * kLog2e);
   }
   const int nt = CAUSAL ? min(nT, (qb * kBlockRows + kBlockRows - 1) / kTile + 1) : nT;
   const int nit = (nt + KS - 1) / KS;
@@ -240,7 +292,6 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   const bf16_t* vbase = P.v + (long)b * T * P.v_stride + hk * D;
   const uint32_t* mbase = DROP ? P.mask + (long)bh * nT * 2 * T : nullptr;   // wave-uniform
   const uint32_t* mrow = DROP ? mbase + (long)h * T + qi : nullptr;
-  const float c = P.scale * kLog2e;
 
   // NST-deep ring of (K, V, dropout-word) stages per key split, filled by compiler-invisible
   // LDS-DMA; a counted vmcnt retires only the stage about to be read and a raw s_barrier
@@ -271,7 +322,12 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   f32x16 oacc[NACC];
 #pragma unroll
   for (int dt = 0; dt < NACC; ++dt) oacc[dt] = f32x16{};
-  float m = -INFINITY, l = 0.f;   // m in scaled log2 units
+  // running max m (scaled log2 units; -inf until this wave's first tile) enters the S chain as its
+  // initial accumulator mv = -m, so S' = (Q c) K^T - m comes out of the MFMAs ready for exp2: the
+  // softmax costs exp + add per probability, plus the packed dropout per pair
+  float m = -INFINITY, l = 0.f;
+  f32x16 mv = f32x16{};
+  bool fresh = true;                             // wave-uniform
 
   for (int it = 0; it < nit; ++it) {
     const int t = it * KS + sp;
@@ -287,69 +343,73 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     const int kv0 = t * kTile;
     if (t < nt && (!CAUSAL || kv0 <= q0 + 31)) {
       f32x16 sacc[2];
+      auto s_tile = [&]() {                        // S' = (Q c) K^T - m
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        sacc[n] = f32x16{};
+        for (int n = 0; n < 2; ++n) {
+          sacc[n] = mv;
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s) sacc[n] = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sacc[n]);
-      }
-      if (CAUSAL && kv0 + kTile - 1 > q0) {        // diagonal tile: mask keys > query
+          for (int s = 0; s < D / 16; ++s) sacc[n] = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sacc[n]);
+        }
+        if (CAUSAL && kv0 + kTile - 1 > q0) {      // diagonal tile: mask keys > query
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              if (kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) sacc[n][i] = -INFINITY;
+        }
+      };
+      auto row_max = [&]() {                       // this tile's row max minus m
+        float mx = sacc[0][0];
 #pragma unroll
         for (int n = 0; n < 2; ++n)
 #pragma unroll
-          for (int i = 0; i < 16; ++i)
-            if (kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) sacc[n][i] = -INFINITY;
-      }
-      float mx = sacc[0][0];
+          for (int i = (n == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, sacc[n][i]);
+        return fmaxf(mx, __shfl_xor(mx, 32, 64));
+      };
+      // move m by d = mx (first tile) or max(mx, 0): rescale l, O and this tile's S'.  Every
+      // visited tile holds at least one unmasked key per row (causal: kv0 <= q0), so mx is finite.
+      auto rescale = [&](float mx) {
+        const float d = fresh ? mx : fmaxf(mx, 0.f);
+        if (!fresh) {
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          l *= alpha;
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int i = (n == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, sacc[n][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c;
-      if (__ballot(mx > m + kRescaleLog2)) {         // wave-uniform, rare after the first tiles
-        const float mnew = fmaxf(m, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
-        m = mnew;
-        l *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
-      }
-#if DLTB_ATTN_PK
-      // packed fp32 (v_pk_fma_f32 / v_pk_add_f32): two probabilities per VALU op
-      typedef float f32x2 __attribute__((ext_vector_type(2)));
-      const f32x2 c2 = {c, c}, nm2 = {-m, -m};
-      f32x2 ls2 = {0.f, 0.f};
-      static_for<16>([&](auto J) {
-        constexpr int n = J / 8, i = 2 * (J % 8);
-        const f32x2 x = __builtin_elementwise_fma(f32x2{sacc[n][i], sacc[n][i + 1]}, c2, nm2);
-        const f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-        ls2 += p;
-        sacc[n][i] = DROP ? keep_and<16 * n + i>(p[0], mw) : p[0];
-        sacc[n][i + 1] = DROP ? keep_and<16 * n + i + 1>(p[1], mw) : p[1];
-      });
-      l += ls2[0] + ls2[1];
-#else
-      const float nm = -m;
-      float ls0 = 0.f, ls1 = 0.f;
-      static_for<32>([&](auto J) {
-        constexpr int n = J / 16, i = J % 16;
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[n][i], c, nm));
-        if constexpr (i & 1) ls1 += p;
-        else ls0 += p;
-        sacc[n][i] = DROP ? keep_and<16 * n + i>(p, mw) : p;
-      });
-      l += ls0 + ls1;
-#endif
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bfx8 pf = pack_frag<D>(sacc[n], s2);
-#pragma unroll
-          for (int dt = 0; dt < NACC; ++dt)
-            oacc[dt] = mfma32(tr_frag<D>(vt, 32 * n + 16 * s2, dt * 32, lane), pf, oacc[dt]);
+          for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
         }
+        m = fresh ? mx : m + d;
+#pragma unroll
+        for (int n = 0; n < 2; ++n) sacc[n] -= d;
+        mv = splat16(-m);
+        fresh = false;
+      };
+      float ls0, ls1;
+      auto exps = [&]() {
+        ls0 = 0.f;
+        ls1 = 0.f;
+        static_for<32>([&](auto J) {
+          constexpr int n = J / 16, i = J % 16;
+          const float p = __builtin_amdgcn_exp2f(sacc[n][i]);
+          if constexpr (i & 1) ls1 += p;
+          else ls0 += p;
+          sacc[n][i] = p;
+        });
+      };
+      s_tile();
+      // lazy rescale: m moves only on the first tile or when a row max exceeds it by more than
+      // kRescaleLog2 (p <= 2^8 in between); wave-uniform, rare after the first tiles
+      {
+        const float mx = row_max();
+        if (fresh || __ballot(mx > kRescaleLog2)) rescale(mx);
       }
+      exps();
+      l += ls0 + ls1;
+      static_for<4>([&](auto J) {
+        constexpr int n = J / 2, s2 = J % 2;
+        const bfx8 pf = pack_frag_keep<n, s2, DROP>(sacc[n], mw);
+#pragma unroll
+        for (int dt = 0; dt < NACC; ++dt)
+          oacc[dt] = mfma32(tr_frag<D>(vt, 32 * n + 16 * s2, dt * 32, lane), pf, oacc[dt]);
+      });
     }
   }
   __syncthreads();              // all LDS reads done before the ring is reused for the merge
@@ -442,11 +502,6 @@ constexpr int dkdv_smem_bytes() {
   return merge > a ? merge : a;
 }
 
-DLTB_DEV float keep_and_v(float p, uint32_t mw, uint32_t bit) {
-  uint32_t k;
-  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(mw), "v"(bit));
-  return __uint_as_float(__float_as_uint(p) & k);
-}
 DLTB_DEV uint32_t keep_mask_v(uint32_t mw, uint32_t bit) {
   uint32_t k;
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(k) : "v"(mw), "v"(bit));
@@ -477,10 +532,9 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const int key = k0 + r;
   // this lane's bit in the packed mask words (see attn_mask_kernel)
   const int hbit = (r >> 2) & 1;
-  const uint32_t jbit = 16 * (kw & 1) + ((r & 3) | (((r >> 3) & 3) << 2));
+  const uint32_t jbit = mask_bit(kw & 1, (r & 3) | (((r >> 3) & 3) << 2));
   const int msub = (kw >> 1) * 2 + hbit;
   const float inv_s = DROP ? 1.f / P.drop_scale : 1.f;
-  const float inv_scale = 1.f / P.scale;
 
   bfx8 kf[D / 16], vf[D / 16];
   {
@@ -488,7 +542,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     const bf16_t* vrow = P.v + ((long)b * T + key) * P.v_stride + hk * D;
 #pragma unroll
     for (int s = 0; s < D / 16; ++s) {
-      kf[s] = __builtin_bit_cast(bfx8, ld16<uint4>(krow + 16 * s + 8 * h));
+      // K c: S' = Q (K c)^T - lse log2(e) is the exp2 argument itself (no multiply per score)
+      kf[s] = scale_frag(__builtin_bit_cast(bfx8, ld16<uint4>(krow + 16 * s + 8 * h)), P.scale * kLog2e);
       vf[s] = __builtin_bit_cast(bfx8, ld16<uint4>(vrow + 16 * s + 8 * h));
     }
   }
@@ -496,7 +551,6 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
 #pragma unroll
   for (int dt = 0; dt < NACC; ++dt) { dk[dt] = f32x16{}; dv[dt] = f32x16{}; }
 
-  const float c = P.scale * kLog2e;
   const int t_begin = CAUSAL ? kblk0 / kTile : 0;
   const int nit = (nT - t_begin + KS - 1) / KS;   // iterations per head
   const int njobs = G * nit;
@@ -528,7 +582,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     GldsTile<D, kTile>::load_sv(P.dout + r0 * P.do_stride + hq * D, doff, base + TB, wv);
     if (stid < kTile) {   // row constants, loaded straight into the S / dP accumulators
       const long rc = bq * T + t * kTile;
-      vl = -P.lse[rc + stid] * inv_scale;
+      vl = -P.lse[rc + stid] * kLog2e;
       vd = -P.delta[rc + stid] * inv_s;
     }
     if (DROP) mword = P.mask[((bq * nT + kb * 2) * 2) * T + t * kTile + moff];
@@ -558,7 +612,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     const float* dlt = lse2 + kTile;
     const uint32_t* mws = reinterpret_cast<const uint32_t*>(dlt + kTile);
     if (j + 1 < njobs) load(j + 1);
-    // S' = Q K^T - lse/scale and dP' = dO V^T - delta/s: p = exp2(c S'), ds = p dP' (no dropout)
+    // S' = Q (K c)^T - lse log2(e) and dP' = dO V^T - delta/s: p = exp2(S'), ds = p dP' (no dropout)
     auto sdp = [&](int mm, f32x16& sa, f32x16& dp) {
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
@@ -605,11 +659,10 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
         }
         const float Dv[4] = {Dl.x, Dl.y, Dl.z, Dl.w};
         const uint32_t Mv[4] = {M4.x, M4.y, M4.z, M4.w};
-#if !DLTB_ATTN_PK
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g4 + e;
-          float p = __builtin_amdgcn_exp2f(sa[i] * c);
+          float p = __builtin_amdgcn_exp2f(sa[i]);
           if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p = 0.f;
           if (DROP) {     // dS = fma(p keep, dP', p D): the masked probability carries the keep bit
             const float pdv = __uint_as_float(__float_as_uint(p) & keep_mask_v(Mv[e], jbit));
@@ -620,36 +673,6 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
             ds[i] = p * dp[i];
           }
         }
-#else
-        // packed fp32 (v_pk_mul / v_pk_add): two scores per VALU op, same roundings
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        const f32x2 c2 = {c, c};
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const int i = 4 * g4 + e;
-          const f32x2 x = f32x2{sa[i], sa[i + 1]} * c2;
-          f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e) p[0] = 0.f;
-          if (CAUSAL && diag && key > qb + 8 * g4 + 4 * h + e + 1) p[1] = 0.f;
-          f32x2 d;
-          if (DROP) {
-            const uint32_t k0m = keep_mask_v(Mv[e], jbit), k1m = keep_mask_v(Mv[e + 1], jbit);
-            // dS = p (keep dP' + D) = fma(p keep, dP', p D): the masked probability (needed for dV
-            // anyway) carries the keep bit, so dP' needs no mask of its own
-            const f32x2 pdv = {__uint_as_float(__float_as_uint(p[0]) & k0m),
-                               __uint_as_float(__float_as_uint(p[1]) & k1m)};
-            pd[i] = pdv[0];
-            pd[i + 1] = pdv[1];
-            d = __builtin_elementwise_fma(pdv, f32x2{dp[i], dp[i + 1]}, p * f32x2{Dv[e], Dv[e + 1]});
-          } else {
-            pd[i] = p[0];
-            pd[i + 1] = p[1];
-            d = p * f32x2{dp[i], dp[i + 1]};
-          }
-          ds[i] = d[0];
-          ds[i + 1] = d[1];
-        }
-#endif
       }
     };
     auto accum = [&](int mm, const f32x16& pd, const f32x16& ds) {
@@ -764,7 +787,7 @@ __global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restric
 // =============================================================================== dQ
 // Query-major, KS key-splits per workgroup as in the forward; dQ partials merge through LDS.
 template <int D>
-constexpr int dq_ks() { return 2; }        // KS = 3 measured neutral at D = 64 (and spills)
+constexpr int dq_ks() { return D == 64 ? DLTB_DQ_KS64 : 2; }
 template <int D>
 constexpr int dq_nst() { return D == 64 ? 3 : 2; }   // LDS ring depth, as the forward's
 template <int D>
@@ -827,12 +850,15 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
   } else {
     dlt = P.delta[bq * T + qi];
   }
-  const float nl = -P.lse[bq * T + qi] / P.scale;                                  // S' = S - lse/scale
-  const float nd = -dlt * (DROP ? 1.f / P.drop_scale : 1.f);                       // dP' = dP - delta/s
+  // row constants as the initial accumulators: S' = (Q c) K^T - lse log2(e) is the exp2 argument
+  // and dP' = dO V^T - delta/s, so p = exp2(S'), dS = p (keep ? dP' : -delta/s)
+  const f32x16 nlv = splat16(-P.lse[bq * T + qi] * kLog2e);
+  const float nd = -dlt * (DROP ? 1.f / P.drop_scale : 1.f);
+  const f32x16 ndv = splat16(nd);
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) qf[s] = scale_frag(qf[s], P.scale * kLog2e);   // after the delta dot
   const uint32_t* mbase = DROP ? P.mask + (long)bq * nT * 2 * T : nullptr;   // wave-uniform
   const uint32_t* mrow = DROP ? mbase + (long)h * T + qi : nullptr;
-  const float c = P.scale * kLog2e;
-  const float nlc = nl * c;
   const int nt = CAUSAL ? min(nT, (qb * kBlockRows + kBlockRows - 1) / kTile + 1) : nT;
   const int nit = (nt + KS - 1) / KS;
   const bf16_t* kbase = P.k + (long)b * T * P.k_stride + hk * D;
@@ -881,8 +907,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
     const int kv0 = t * kTile;
     // S^T / dP^T of key sub-tile n (32 keys x this wave's 32 queries)
     auto sdp = [&](int n, f32x16& sa, f32x16& dp) {
-      sa = f32x16{};
-      dp = f32x16{};
+      sa = nlv;
+      dp = ndv;
 #pragma unroll
       for (int s = 0; s < D / 16; ++s) {
         sa = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sa);
@@ -893,32 +919,14 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
     auto fin = [&](int n, const f32x16& sa, const f32x16& dp) {
       const bool diag = CAUSAL && kv0 + 32 * n + 31 > q0;
       f32x16 ds;
-#if !DLTB_ATTN_PK
       static_for<16>([&](auto I) {
         constexpr int i = I;
-        float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sa[i], c, nlc));
+        float p = __builtin_amdgcn_exp2f(sa[i]);
         if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p = 0.f;
-        const float dpv = DROP ? (n == 0 ? keep_and<i>(dp[i], mw) : keep_and<16 + i>(dp[i], mw)) : dp[i];
-        ds[i] = p * (dpv + nd);
+        const float dpv = DROP ? (n == 0 ? keep_sel<mask_bit(0, i)>(dp[i], nd, mw)
+                                         : keep_sel<mask_bit(1, i)>(dp[i], nd, mw)) : dp[i];
+        ds[i] = p * dpv;
       });
-#else
-      // packed fp32 (v_pk_fma / v_pk_add / v_pk_mul): two scores per VALU op, same roundings
-      typedef float f32x2 __attribute__((ext_vector_type(2)));
-      const f32x2 c2 = {c, c}, nl2 = {nlc, nlc}, nd2 = {nd, nd};
-      static_for<8>([&](auto J) {
-        constexpr int i = 2 * J;
-        const f32x2 x = __builtin_elementwise_fma(f32x2{sa[i], sa[i + 1]}, c2, nl2);
-        f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
-        if (diag && kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) p[0] = 0.f;
-        if (diag && kv0 + 32 * n + ((i + 1) & 3) + 8 * ((i + 1) >> 2) + 4 * h > qi) p[1] = 0.f;
-        const f32x2 dpv = DROP ? (n == 0 ? f32x2{keep_and<i>(dp[i], mw), keep_and<i + 1>(dp[i + 1], mw)}
-                                         : f32x2{keep_and<16 + i>(dp[i], mw), keep_and<17 + i>(dp[i + 1], mw)})
-                               : f32x2{dp[i], dp[i + 1]};
-        const f32x2 d = p * (dpv + nd2);
-        ds[i] = d[0];
-        ds[i + 1] = d[1];
-      });
-#endif
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const bfx8 sf = pack_frag<D>(ds, s2);

@@ -3,12 +3,21 @@
 // first LayerNorm: the VALU-bound hash and the latency-bound row norm fill each other's idle
 // issue slots).
 //
-// word (bh, t, h, q) at ((bh*nT + t)*2 + h)*T + q; bit 16n + i <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h
-// (the lane layout of the attention kernels' S tiles; see attention.hip).
+// word (bh, t, h, q) at ((bh*nT + t)*2 + h)*T + q; bit mask_bit(n, i) <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h
+// (the lane layout of the attention kernels' S tiles; see attention.hip).  Score pair j = 8n + (i>>1)
+// (the two probabilities one v_cvt_pk_bf16_f32 packs) sits at bits 15 - j (even i) and 31 - j (odd i):
+// after a left shift by j both are sign bits of their 16-bit halves, so one v_perm_b32 turns them
+// into the pair's 0x0000/0xFFFF keep masks and the forward drops probabilities on the packed bf16
+// P operand (shift + perm + and per PAIR instead of bfe + and per score).
 #pragma once
 #include "common.h"
 
 constexpr int kMaskKeyTile = 64;   // keys per packed tile (attention.hip kTile)
+
+// bit of score register i (0..15) of key sub-tile n (0, 1) in a packed keep word
+constexpr uint32_t mask_bit(int n, int i) {
+  return (uint32_t)((i & 1) ? 31 - (8 * n + (i >> 1)) : 15 - (8 * n + (i >> 1)));
+}
 
 // one thread = one query row q of tile group g = (bh * nT + t) * 2 + h; 32 keep decisions
 DLTB_DEV void attn_mask_word(uint32_t* __restrict__ mask, int T, uint32_t thr16, const int64_t* __restrict__ seed_ptr,
@@ -27,8 +36,8 @@ DLTB_DEV void attn_mask_word(uint32_t* __restrict__ mask, int T, uint32_t thr16,
     for (int i = 0; i < 16; i += 2) {
       const uint32_t key = (uint32_t)(t * kMaskKeyTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
       const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
-      bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << (16 * n + i);
-      bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << (16 * n + i + 1);
+      bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << mask_bit(n, i);
+      bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << mask_bit(n, i + 1);
     }
   mask[(size_t)g * T + q] = bits;
 }

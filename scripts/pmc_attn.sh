@@ -5,6 +5,7 @@ set -uo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 OUT="${1:-$ROOT/gpurun_out/pmc_attn}"
 mkdir -p "$OUT"
+OUT="$(cd "$OUT" && pwd)"          # absolute: the profiler runs from /tmp
 cd /tmp && export TMPDIR=/tmp
 pass() {
   local name="$1"; shift

@@ -382,7 +382,11 @@ def test_attention(B, T, Hq, Hkv, D, causal, p):
     amask = C.attn_mask(B, T, Hq, p, sd.device_tensor, 11, q) if p else None
     o, lse = C.attn_fwd(q, k, v, amask, B, T, Hq, Hkv, scale, causal, p)
     ro, rlse = ref.attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, sd, 11)
-    close(lse, rlse, 2e-3, 1e-3, "lse")
+    # the kernels form the scores from Q * scale * log2(e) rounded to bf16 once per element (the
+    # softmax scale folded into the operand): |score error| <= ~2^-9 |score|, the rounding the
+    # reference's own bf16 bmm applies to every score (torch MHA under autocast).  A causal row with
+    # one visible key has lse = that score, so the absolute lse tolerance is a few 2^-9 |score|.
+    close(lse, rlse, 8e-3, 1e-3, "lse")
     close(o, ro, 2e-2, 3e-2, "O")
     do = rnd(B * T, Hq * D)
     dqkv = torch.empty_like(qkv)
