@@ -300,13 +300,13 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   constexpr int SB = fwd_stage_bytes<D>();
   constexpr int GL = 2 * GldsTile<D, kTile>::NI + (DROP ? 1 : 0);   // DMA instructions per stage
   const int wv = __builtin_amdgcn_readfirstlane(qw);
-  auto stage_ptr = [&](int it) { return smem + ((it % NST) * KS + sp) * SB; };
+  const int spu = __builtin_amdgcn_readfirstlane(sp);      // the key split is wave-uniform
+  auto stage_ptr = [&](int it) { return smem + ((it % NST) * KS + spu) * SB; };
   // per-lane DMA offsets are tile-invariant; the tile's row goes into the SGPR base (SALU only)
   uint32_t koff[GldsTile<D, kTile>::NI], voff[GldsTile<D, kTile>::NI];
   GldsTile<D, kTile>::offsets(P.k_stride, wv, lane, koff);
   GldsTile<D, kTile>::offsets(P.v_stride, wv, lane, voff);
   const uint32_t moff = (uint32_t)(mrow - mbase) * 4u;
-  const int spu = __builtin_amdgcn_readfirstlane(sp);      // the key split is wave-uniform
   auto issue = [&](int it) {
     const int t = it * KS + spu;
     if (it >= nit || t >= nt) return;
@@ -330,10 +330,10 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   bool fresh = true;                             // wave-uniform
 
   for (int it = 0; it < nit; ++it) {
-    const int t = it * KS + sp;
+    const int t = it * KS + spu;                   // wave-uniform: the tile branches are scalar
     // stage it+1 (issued only if its tile exists for this split) may stay in flight
     static_assert(NST <= 3, "the counted wait below assumes at most one later stage in flight");
-    if (NST > 2 && it + 1 < nit && (it + 1) * KS + sp < nt) wait_vm<(NST > 2 ? GL : 0)>();
+    if (NST > 2 && it + 1 < nit && (it + 1) * KS + spu < nt) wait_vm<(NST > 2 ? GL : 0)>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     issue(it + NST - 1);                         // refills the buffer read in iteration it - 1
@@ -343,13 +343,13 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     const int kv0 = t * kTile;
     if (t < nt && (!CAUSAL || kv0 <= q0 + 31)) {
       f32x16 sacc[2];
-      auto s_tile = [&]() {                        // S' = (Q c) K^T - m
+      auto s_tile = [&]() {                        // S' = (Q c) K^T - m, the two key halves interleaved
+        sacc[0] = mfma32(row_frag<D>(kt, r, h), qf[0], mv);
+        sacc[1] = mfma32(row_frag<D>(kt, 32 + r, h), qf[0], mv);
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          sacc[n] = mv;
+        for (int s = 1; s < D / 16; ++s)
 #pragma unroll
-          for (int s = 0; s < D / 16; ++s) sacc[n] = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sacc[n]);
-        }
+          for (int n = 0; n < 2; ++n) sacc[n] = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sacc[n]);
         if (CAUSAL && kv0 + kTile - 1 > q0) {      // diagonal tile: mask keys > query
 #pragma unroll
           for (int n = 0; n < 2; ++n)
@@ -364,7 +364,9 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
         for (int n = 0; n < 2; ++n)
 #pragma unroll
           for (int i = (n == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, sacc[n][i]);
-        return fmaxf(mx, __shfl_xor(mx, 32, 64));
+        // the other half of the row sits in lane ^ 32: one v_permlane32_swap, no LDS round trip
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       };
       // move m by d = mx (first tile) or max(mx, 0): rescale l, O and this tile's S'.  Every
       // visited tile holds at least one unmasked key per row (causal: kv0 <= q0), so mx is finite.

@@ -29,15 +29,25 @@ DLTB_DEV void attn_mask_word(uint32_t* __restrict__ mask, int T, uint32_t thr16,
   const uint32_t bh = (g >> 1) / nT;
   const uint64_t seed = site_seed(seed_ptr, site);
   const uint32_t rk = rng_row_key(seed, bh * (uint32_t)T + q);
-  uint32_t bits = 0;
+  uint32_t bits = 0xFFFFFFFFu;                               // thr16 == 0: keep everything
+  if (thr16 != 0) {
+    // one hash covers a key pair (i, i+1) of register pair j = 8n + i/2, whose keep bits live at
+    // 15 - j and 31 - j: both 16-bit halves compared at once, (h - (thr - 1)) saturated then
+    // min'ed with 1 gives 0 / 1 per half, shifted into place by one v_lshl_or_b32
+    const uint32_t tm2 = (thr16 - 1u) * 0x10001u, one2 = 0x10001u;
+    bits = 0;
 #pragma unroll
-  for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      const uint32_t key = (uint32_t)(t * kMaskKeyTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
-      const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
-      bits |= (keep_lo(hsh, thr16) ? 1u : 0u) << mask_bit(n, i);
-      bits |= (keep_hi(hsh, thr16) ? 1u : 0u) << mask_bit(n, i + 1);
-    }
+      for (int i = 0; i < 16; i += 2) {
+        const uint32_t key = (uint32_t)(t * kMaskKeyTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
+        const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
+        uint32_t kk;
+        asm("v_pk_sub_u16 %0, %1, %2 clamp\n\tv_pk_min_u16 %0, %0, %3"
+            : "=&v"(kk) : "v"(hsh), "v"(tm2), "v"(one2));
+        static_assert(mask_bit(0, 1) == mask_bit(0, 0) + 16, "pair bits 16 apart");
+        bits |= kk << mask_bit(n, i);
+      }
+  }
   mask[(size_t)g * T + q] = bits;
 }

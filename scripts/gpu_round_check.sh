@@ -13,5 +13,7 @@ for r in 1 2; do
 done
 bash scripts/rocprof.sh gpurun_out/prof_steady > gpurun_out/rocprof.log 2>&1
 head -20 gpurun_out/prof_steady/summary_steady.txt
-bash scripts/pmc_attn.sh gpurun_out/pmc_attn > gpurun_out/pmc_attn.txt 2>&1
-cat gpurun_out/pmc_attn.txt | grep -A1 "attn_fwd\|attn_bwd_dq\|attn_bwd_dkdv" | head -30
+if [ "${PMC:-0}" = 1 ]; then
+  bash scripts/pmc_attn.sh gpurun_out/pmc_attn > gpurun_out/pmc_attn.txt 2>&1
+  grep -A1 "attn_fwd\|attn_bwd_dq\|attn_bwd_dkdv" gpurun_out/pmc_attn.txt | head -30
+fi
