@@ -284,12 +284,18 @@ def scale_by(x, num, den=None):
 
 
 def head_dgrad(dl, w, wt, g):
-    """dX = g * dL W for an LM head with weight W [V, d].  On MI355X with a cached W^T this is the
-    split-K MFMA GEMM (NT form, g applied as a device alpha in the split-K reduction): K = V is
-    long and the output (tokens x d) small, which hipBLASLt's NN kernels handle poorly."""
+    """dX = g * dL W for an LM head with weight W [V, d].  K = V is long and the output (tokens x d)
+    small.  With a cached W^T both operands are K-contiguous: a tuned hipBLASLt split-K solution
+    when the table has the problem (TinyGPT-A: 116 us vs 149 us for the own kernel + reduce,
+    profiles/head_dgrad_blaslt_r2.txt), then g applied by one small scale kernel; otherwise the
+    own split-K MFMA GEMM with g as a device alpha in its split-K reduction."""
     if _gpu(dl) and wt is not None and dl.stride(1) == 1 and dl.dtype == torch.bfloat16:
         M, K = dl.shape
         N = wt.shape[0]
+        if _blt.active():
+            dh = torch.empty(M, N, dtype=dl.dtype, device=dl.device)
+            if _blt.mm(dl, wt.t(), dh, False):
+                return ext().scale_by(dh, g, None, None)
         C = ext()
         if C.gemm_supported(M, N, K, False, 2):
             return C.gemm(dl, wt, None, None, False, False, 4, 2, 0, 1, g)

@@ -148,3 +148,23 @@ def test_wgrad_transposed_operand(which):
     check(dw, 2 * want, "accumulate")
     small = F_.wgrad_operands(rnd(2048, 1024), rnd(2048, 1024))             # small product: untouched
     assert small[1].stride(1) == 1 and not small[0].is_contiguous()
+
+
+def test_head_dgrad_table_path():
+    """TinyGPT-A's tied-head dgrad (2048 x 32000 x 1024, K = vocab) dispatches to the shipped table's
+    split-K hipBLASLt entry with the device-scalar g applied afterwards, and matches g * dL W."""
+    from dltb.ops import functional as F_
+    blaslt.load()
+    dl, wte = rnd(2048, 32000), rnd(32000, 1024)
+    wt = wte.t().contiguous()
+    g = torch.tensor([0.37], device="cuda")
+    dh0 = torch.empty(2048, 1024, device="cuda", dtype=BF)
+    assert blaslt.problem(dl, wt.t(), dh0, False) is not None
+    got = F_.head_dgrad(dl, wte, wt, g)
+    want = (dl.float() @ wte.float()) * 0.37
+    check(got, want, "head dgrad (table)")
+    blaslt.disable()
+    try:
+        check(F_.head_dgrad(dl, wte, wt, g), want, "head dgrad (own split-K kernel)")
+    finally:
+        blaslt.load()
