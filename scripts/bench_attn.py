@@ -20,7 +20,9 @@ from dltb.ops._ext import ext  # noqa: E402
 
 SHAPES = {"tinygpt_a": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.1),
           "tinygpt_a_p0": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.0),
-          "m7b": dict(B=1, T=4096, Hq=32, Hkv=8, D=128, causal=True, p=0.0)}
+          "m7b": dict(B=1, T=4096, Hq=32, Hkv=8, D=128, causal=True, p=0.0),
+          # three TinyGPT-A micro-batches: 768 query blocks, so several workgroups share a CU
+          "tinygpt_a_b3": dict(B=3, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.1)}
 
 
 def timeit(fn, iters):
