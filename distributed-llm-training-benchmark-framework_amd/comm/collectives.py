@@ -23,7 +23,14 @@ engines own their communication, and this module is the one place that talks to
   per-bucket batched weight gradients, deferred all-gathers waited in ``acquire``, fp32
   accumulation of reduce-scattered chunks, ZeRO-3 transient gather buffers) runs with the real
   HIP kernels.  It is a correctness mode, not a performance mode.
+* Lazy mode (``DLTB_COMM_LAZY=1``, tests): an asynchronous collective runs only when its work is
+  waited -- it reads its input and writes its output at ``wait()``, the latest moment RCCL could.
+  A rank that overwrites a buffer still being reduced, reads a result before waiting for it, or
+  never waits at all then computes different numbers, so the world-size equivalence tests catch
+  missing or misplaced waits deterministically (the host-staged and CPU gloo paths are otherwise
+  synchronous or racy, and only RCCL on several GPUs runs truly asynchronously).
 """
+import os
 from collections import OrderedDict
 
 import torch
@@ -41,6 +48,22 @@ class _Done:
 
 
 _DONE = _Done()
+
+
+class _Lazy:
+    """Work whose collective runs at the first ``wait()`` (lazy mode)."""
+
+    def __init__(self, fn):
+        self._fn = fn
+
+    def wait(self):
+        if self._fn is not None:
+            fn, self._fn = self._fn, None
+            fn()
+        return True
+
+    def is_completed(self):
+        return self._fn is None
 
 _REDUCE_OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "avg": "AVG"}
 
@@ -62,6 +85,7 @@ class Comm:
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.backend = dist.get_backend(group) if self.enabled else "none"
         self.staged = self.backend == "gloo"      # device tensors go through host memory
+        self.lazy = os.environ.get("DLTB_COMM_LAZY", "0") == "1"
         self._pending = []
         self.stats = OrderedDict()            # op -> {"calls": n, "wire_bytes": b}
 
@@ -105,11 +129,23 @@ class Comm:
             dst.copy_(h)
 
     # ------------------------------------------------------------------ collectives
+    def _lazy(self, fn, async_op: bool, track: bool):
+        if not async_op:
+            fn()
+            return _DONE
+        w = _Lazy(fn)
+        return self._track(w, True) if track else w
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = True, track: bool = True):
         """In-place all-reduce of a flat buffer slice (DDP bucket, grad-norm scalar)."""
         if self.world == 1:
             return _DONE
         self._count("all_reduce", t)
+        if self.lazy:
+            return self._lazy(lambda: self._all_reduce(t, op), async_op, track)
+        return self._all_reduce(t, op, async_op, track)
+
+    def _all_reduce(self, t, op, async_op=False, track=True):
         if self.staged and t.is_cuda:
             h = self._host(t)
             dist.all_reduce(h, op=getattr(dist.ReduceOp, _REDUCE_OPS[op]), group=self.group)
@@ -128,6 +164,11 @@ class Comm:
             return _DONE
         assert inp.numel() == out.numel() * self.world, "reduce_scatter: input must be world x output"
         self._count("reduce_scatter", inp)
+        if self.lazy:
+            return self._lazy(lambda: self._reduce_scatter(out, inp), async_op, track)
+        return self._reduce_scatter(out, inp, async_op, track)
+
+    def _reduce_scatter(self, out, inp, async_op=False, track=True):
         if self.staged and (inp.is_cuda or out.is_cuda):
             h = torch.empty(out.shape, dtype=out.dtype)
             dist.reduce_scatter_tensor(h, self._host(inp), group=self.group)
@@ -146,6 +187,11 @@ class Comm:
             return _DONE
         assert out.numel() == inp.numel() * self.world, "all_gather: output must be world x input"
         self._count("all_gather", out)
+        if self.lazy:
+            return self._lazy(lambda: self._all_gather(out, inp), async_op, track)
+        return self._all_gather(out, inp, async_op, track)
+
+    def _all_gather(self, out, inp, async_op=False, track=True):
         if self.staged and (inp.is_cuda or out.is_cuda):
             h = torch.empty(out.shape, dtype=out.dtype)
             dist.all_gather_into_tensor(h, self._host(inp), group=self.group)

@@ -29,8 +29,9 @@ def resolve_ranks(world_size=None, rank=None, local_rank=None):
 
 
 def setup_distributed(world_size, rank, local_rank, master_addr=None, master_port=None,
-                      device_type="cuda", timeout_min=30, debug_collectives=False):
-    """Initialise the process group when world_size > 1; returns the torch.device of this rank."""
+                      device_type="cuda", timeout_min=30, debug_collectives=False, force_pg=False):
+    """Initialise the process group when world_size > 1 (or ``force_pg``: a one-rank group, which
+    runs the RCCL init options and collectives on a one-GPU box); returns this rank's torch.device."""
     host_comm = device_type == "cuda" and os.environ.get("DLTB_COMM", "rccl") == "host"
     if device_type == "cuda":
         if not torch.cuda.is_available():
@@ -41,7 +42,7 @@ def setup_distributed(world_size, rank, local_rank, master_addr=None, master_por
         device = torch.device("cuda", local_rank)
     else:
         device = torch.device("cpu")
-    if world_size > 1 and not dist.is_initialized():
+    if (world_size > 1 or force_pg) and not dist.is_initialized():
         if debug_collectives:
             os.environ["TORCH_DISTRIBUTED_DEBUG"] = "DETAIL"
         if master_addr:

@@ -24,3 +24,10 @@ def test_world2_host_staged_equals_world1_gpu(tmp_path):
                env_extra={"DLTB_COMM": "host", "DLTB_DEFER_OPT": "0"}, timeout=600)
     bad = compare({k: ws1[k] for k in ws2n}, ws2n, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
     assert not bad, bad
+    # DLTB_COMM_LAZY=1: every asynchronous collective reads its input and writes its output only
+    # at its wait() (comm/collectives.py), so a missing or misplaced wait in the bf16 GPU paths
+    # (per-bucket batched dW before the reduce-scatter, reduce-scatters left in flight across
+    # micro-steps, deferred all-gathers waited in acquire, ZeRO-3 prefetch) changes the result
+    ws2l = run(tmp_path / "ws2l.pt", 2, "cuda", env_extra={"DLTB_COMM": "host", "DLTB_COMM_LAZY": "1"}, timeout=600)
+    bad = compare({k: ws1[k] for k in ws2l}, ws2l, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
+    assert not bad, bad

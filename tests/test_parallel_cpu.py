@@ -219,3 +219,34 @@ def test_zero3_288gb_config_keeps_gathered_params():
     e = make_engine(m, engine_config("zero3", 2, "reference", ds_config=big), "cpu")
     assert e.keep_all
     json.dumps(big)
+
+
+def _worker_lazy(rank, *args):
+    os.environ["DLTB_COMM_LAZY"] = "1"        # every async collective runs at its wait()
+    _worker(rank, *args)
+
+
+@pytest.mark.parametrize("strategy,accum,kw", [
+    ("ddp", 1, {}),
+    ("ddp", 2, {"semantics": "uniform"}),
+    ("zero2", 2, {}),
+    ("zero2", 2, {"zero_stage": 1}),
+    ("zero3", 2, {}),
+    ("zero3", 1, {"max_live": 0}),
+    ("fsdp", 1, {}),
+    ("fsdp", 2, {"semantics": "uniform"}),
+])
+def test_world2_lazy_collectives_match_single_process(strategy, accum, kw):
+    """Wait discipline: with DLTB_COMM_LAZY=1 a collective reads its input and writes its output
+    only when its work is waited (the latest point RCCL could), so a buffer reused before the
+    collective finished, a result read before its wait, or a work never waited changes the trained
+    weights.  Deferred reduce-scatters across micro-steps, deferred parameter all-gathers waited in
+    ``acquire`` and ZeRO-3 / FSDP prefetches must all still reproduce the single-process run."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "sd.pt")
+        mp.spawn(_worker_lazy, args=(world, _free_port(), strategy, accum, dict(kw), out), nprocs=world, join=True)
+        got = torch.load(out, weights_only=True)
+    ref = _train(strategy, _batches(STEPS, 4), 0, 1, accum, **dict(kw))
+    for n in ref:
+        assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
