@@ -500,3 +500,30 @@ def test_norm_fwd_mask_fused_matches_separate(with_res):
     if with_res:
         assert torch.equal(s0, s1)
     assert torch.equal(mk0, mk1)
+
+
+def test_attn_mask_words_match_reference():
+    """The packed attention-dropout words are bit-exact with ops/rng.py keep_mask: word
+    (bh, t, h, q) bit mask_bit(n, i) <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h (csrc/attn_mask.h)."""
+    from dltb.ops import rng
+    C = ext()
+    B, T, H, p, site = 2, 256, 3, 0.1, 13
+    sd = seed_obj(2024)
+    q = rnd(B * T, H * 64)
+    words = C.attn_mask(B, T, H, p, sd.device_tensor, site, q).view(B * H, T // 64, 2, T)
+    u = words.to(torch.int64) & 0xFFFFFFFF
+    bit = torch.arange(32, device=DEV)
+    j = torch.where(bit < 16, 15 - bit, 31 - bit)                 # pair index of each bit
+    i = 2 * (j & 7) + (bit >= 16).to(torch.int64)
+    n = j >> 3
+    got = torch.empty(B * H, T, T, dtype=torch.bool, device=DEV)
+    for t in range(T // 64):
+        for h in range(2):
+            keys = 64 * t + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h          # [32]
+            bits = ((u[:, t, h, :, None] >> bit) & 1).bool()                 # [BH, T(q), 32]
+            got[:, :, keys] = bits
+    s = rng.site_seed(int(sd.value), site)
+    rows = torch.arange(B * H * T, dtype=torch.int64, device=DEV)[:, None]
+    cols = torch.arange(T, dtype=torch.int64, device=DEV)[None, :]
+    want = rng.keep_mask(s, rows, cols, p).view(B * H, T, T)
+    assert torch.equal(got, want)
