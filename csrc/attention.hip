@@ -315,6 +315,14 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     GldsTile<D, kTile>::load_sv(vbase + (long)t * kTile * P.v_stride, voff, st + TB, wv);
     if (DROP) glds4_sv(mbase + (long)t * 2 * T, moff, st + 2 * TB + wv * 256);
   };
+  // loop-invariant lane offsets of the LDS fragment reads (K rows per k-step, V^T per D tile/half)
+  uint32_t kfo[D / 16], vfo[NACC][2];
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) kfo[s] = row_lane_off<D>(r, 2 * s + h);
+#pragma unroll
+  for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) vfo[dt][hf] = tr_lane_off<D>(dt * 32, hf, lane);
   wait_vm<0>();        // Q fragments landed: no compiler vmcnt wait for them inside the loop
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i) issue(i);
@@ -344,12 +352,17 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
     if (t < nt && (!CAUSAL || kv0 <= q0 + 31)) {
       f32x16 sacc[2];
       auto s_tile = [&]() {                        // S' = (Q c) K^T - m, the two key halves interleaved
-        sacc[0] = mfma32(row_frag<D>(kt, r, h), qf[0], mv);
-        sacc[1] = mfma32(row_frag<D>(kt, 32 + r, h), qf[0], mv);
+        const uint32_t kb = __builtin_amdgcn_readfirstlane(lds_addr(kt));
+        uint32_t ka[D / 16];
 #pragma unroll
-        for (int s = 1; s < D / 16; ++s)
-#pragma unroll
-          for (int n = 0; n < 2; ++n) sacc[n] = mfma32(row_frag<D>(kt, 32 * n + r, 2 * s + h), qf[s], sacc[n]);
+        for (int s = 0; s < D / 16; ++s) ka[s] = lane_addr(kb, kfo[s]);
+        sacc[0] = mfma32(row_frag_at<0>(ka[0]), qf[0], mv);
+        sacc[1] = mfma32(row_frag_at<32 * D * 2>(ka[0]), qf[0], mv);
+        static_for<D / 16 - 1>([&](auto S1) {
+          constexpr int s = S1 + 1;
+          sacc[0] = mfma32(row_frag_at<0>(ka[s]), qf[s], sacc[0]);
+          sacc[1] = mfma32(row_frag_at<32 * D * 2>(ka[s]), qf[s], sacc[1]);
+        });
         if (CAUSAL && kv0 + kTile - 1 > q0) {      // diagonal tile: mask keys > query
 #pragma unroll
           for (int n = 0; n < 2; ++n)
@@ -405,12 +418,18 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
       }
       exps();
       l += ls0 + ls1;
+      const uint32_t vb = __builtin_amdgcn_readfirstlane(lds_addr(vt));
+      uint32_t va[NACC][2];
+#pragma unroll
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) va[dt][hf] = lane_addr(vb, vfo[dt][hf]);
       static_for<4>([&](auto J) {
         constexpr int n = J / 2, s2 = J % 2;
         const bfx8 pf = pack_frag_keep<n, s2, DROP>(sacc[n], mw);
 #pragma unroll
         for (int dt = 0; dt < NACC; ++dt)
-          oacc[dt] = mfma32(tr_frag<D>(vt, 32 * n + 16 * s2, dt * 32, lane), pf, oacc[dt]);
+          oacc[dt] = mfma32(tr_frag_at<(32 * n + 16 * s2) * D * 2>(va[dt][0], va[dt][1]), pf, oacc[dt]);
       });
     }
   }

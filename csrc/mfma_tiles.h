@@ -62,6 +62,45 @@ DLTB_DEV bfx8 tr_frag(const char* tile, int row_base, int col_base, int lane) {
   return __builtin_bit_cast(bfx8, c);
 }
 
+// Hoisted addressing.  The swizzle only reads row bits 0..3, so a fragment whose tile row is
+// (multiple of 16) + (lane part) has the byte offset  16-row-aligned base * (2 D) + lane offset:
+// the lane offset is loop-invariant (a VGPR computed once), the row base a compile-time constant
+// the compiler folds into the ds_read's immediate offset field.  Per tile that leaves one VALU add
+// per distinct lane offset (stage base + offset) instead of address arithmetic per LDS read.
+template <int D>
+DLTB_DEV uint32_t row_lane_off(int lane_row, int ch) { return (uint32_t)toff<D>(lane_row, ch); }
+template <int D>
+DLTB_DEV uint32_t tr_lane_off(int col_base, int half, int lane) {   // tr_frag's p0 (half 0) / p1 (half 1)
+  const int g = lane >> 4, i = lane & 15;
+  const int row = 4 * (g >> 1) + (i >> 2) + 8 * half;
+  const int col = col_base + 16 * (g & 1) + 4 * (i & 3);
+  return (uint32_t)(toff<D>(row, col >> 3) + (col & 7) * 2);
+}
+typedef __attribute__((address_space(3))) const char lds_cchar;
+typedef __attribute__((address_space(3))) const uint4 lds_u4;
+// 32-bit LDS address of a pointer into dynamic shared memory
+DLTB_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(size_t)(lds_cchar*)p; }
+// stage base (wave-uniform, SGPR) + lane offset in one v_add the compiler cannot re-associate: the
+// fragment reads below then carry their row constants in the ds_read immediate offset instead of a
+// per-read subtract + add chain (LSR re-derives one address per read otherwise)
+DLTB_DEV uint32_t lane_addr(uint32_t sbase, uint32_t off) {
+  uint32_t a;
+  asm("v_add_u32 %0, %1, %2" : "=v"(a) : "s"(sbase), "v"(off));
+  return a;
+}
+template <int OFF>
+DLTB_DEV bfx8 row_frag_at(uint32_t a) { return __builtin_bit_cast(bfx8, *(lds_u4*)(size_t)(a + OFF)); }
+// tr_frag(tile, row_base, col_base, lane) == tr_frag_at<row_base * 2 D>(base + tr_lane_off(col_base, 0),
+// base + tr_lane_off(col_base, 1)) for row_base % 16 == 0
+template <int OFF>
+DLTB_DEV bfx8 tr_frag_at(uint32_t a0, uint32_t a1) {
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(a0 + OFF));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(size_t)(a1 + OFF));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bfx8, c);
+}
+
 // ROWS-row tile of D-element rows filled by LDS-DMA from a row-major global matrix (rows
 // row0 .. row0 + ROWS - 1, columns col0 .. col0 + D - 1 of `base`, row stride `stride`) by 4 waves.
 // Completion: a __syncthreads() (which waits vmcnt(0)) before anyone reads the tile.
