@@ -1,6 +1,9 @@
 #!/usr/bin/env bash
 # Full benchmark suite on one 8x MI355X node: every strategy at 1/2/4/8 GPUs (reference:
 # scripts/run_all_benchmarks.sh ran {ddp,fsdp,zero2,zero3} x WS{2,4} as K8s jobs).
+#  0. RCCL correctness (real GPUs, >= 2 visible): scripts/rccl_equivalence.py trains every engine
+#     at the largest and smallest multi-GPU world sizes of WS_LIST over RCCL and against one rank on
+#     the concatenated batch -> summary/rccl_equivalence.json (RCCL_CHECK=0 skips it).
 #  1. xGMI collective sweep (scripts/bench_collectives.py) at every multi-GPU world size ->
 #     summary/xgmi_buckets.json (and profiles/xgmi_buckets.json on real GPUs), which
 #     comm/topology.py reads to size the gradient buckets of every following run.
@@ -34,6 +37,18 @@ export HSA_ENABLE_IPC_MODE_LEGACY="${HSA_ENABLE_IPC_MODE_LEGACY:-0}"
 echo "=================================================================="
 echo "  MI355X Distributed Training Benchmark Suite ($NGPU GPUs visible)"
 echo "=================================================================="
+
+# ---- 0. RCCL correctness: every engine at N ranks == 1 rank on the concatenated batch
+if [[ "${RCCL_CHECK:-1}" != "0" && -z "${FORCE_NPROC:-}" && "$NGPU" -ge 2 ]]; then
+  RWS=(); for ws in $WS_LIST; do [[ "$ws" -ge 2 && "$ws" -le "$NGPU" ]] && RWS+=("$ws"); done
+  if [[ ${#RWS[@]} -gt 0 ]]; then
+    CHK=("${RWS[0]}"); [[ ${#RWS[@]} -gt 1 ]] && CHK+=("${RWS[-1]}")
+    echo "---- RCCL equivalence ws=${CHK[*]}"
+    timeout -k 30 "$((3 * TIMEOUT))" python3 "$ROOT/scripts/rccl_equivalence.py" --ws "${CHK[@]}" \
+      --out "$RESULTS/summary/rccl_equivalence.json" > "$RESULTS/rccl_equivalence.log" 2>&1 \
+      || { FAILED+=("rccl-equivalence"); echo "     FAILED (see $RESULTS/rccl_equivalence.log)"; }
+  fi
+fi
 
 # ---- 1. collective sweep -> bucket sizing profile
 PROFILE="$RESULTS/summary/xgmi_buckets.json"
