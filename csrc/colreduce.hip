@@ -142,10 +142,16 @@ __global__ __launch_bounds__(256) void colreduce_multi_kernel(ColRedArgs A) {
 
 }  // namespace
 
+#ifndef DLTB_COLPART_RPP
+#define DLTB_COLPART_RPP 16     // rows per partial (per workgroup)
+#endif
+#ifndef DLTB_COLPART_PMAX
+#define DLTB_COLPART_PMAX 128   // partial rows at most
+#endif
 int dltb_colpart_partials(int N) {
-  int P = N / 16;
+  int P = N / DLTB_COLPART_RPP;
   if (P < 1) P = 1;
-  if (P > 128) P = 128;
+  if (P > DLTB_COLPART_PMAX) P = DLTB_COLPART_PMAX;
   return P;
 }
 
