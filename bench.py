@@ -244,7 +244,9 @@ def run_rank(args) -> int:
                 "wire_bytes_per_step_model": engine.comm_bytes_per_step,
                 "tflops_per_gpu": value / world * flops / 1e12,
                 "mfu_dense_bf16": value / world * flops / 2.5e15,
-                "baseline_note": "vs_baseline = value / 18147 tok/s (reference best: ZeRO-2 on 4x A10, BASELINE.md)",
+                "baseline_note": "vs_baseline = value / 18147 tok/s (reference best: ZeRO-2 on 4x A10, BASELINE.md); "
+                                 "vs_baseline_per_gpu = (value / n_gpus) / (18147 / 4), the per-GPU ratio",
+                "vs_baseline_per_gpu": (value / world) / (BASELINE_TPS / 4) if (args.tier == "A" and args.seq_len == 2048) else None,
                 "same_strategy_published": same,
                 "gemm_tuning": tmode,
                 "hip_graphs": graphed,
