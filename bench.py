@@ -238,7 +238,7 @@ def run_rank(args) -> int:
                 "mean_loss": mean_loss,
                 "final_loss": final_loss,
                 "peak_hbm_gb": peak_gb,
-                "trainable_params": sum(p.numel() for p in model.parameters() if p.requires_grad),
+                "trainable_params": mcfg.num_params(),   # every parameter trains (config count: sharded engines free storage)
                 "comm_wait_ms": comm_wait if phases else None,
                 "phase_ms": phases,
                 "wire_bytes_per_step": wire,
