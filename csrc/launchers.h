@@ -13,7 +13,8 @@ void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, v
 void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void* b, void* s_out, void* y,
                         float* mean, float* rstd, int N, int d, float eps, bool rms, uint32_t thr16,
                         float drop_scale, const int64_t* seed, int64_t site, uint32_t* mask, int B, int T,
-                        int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st);
+                        int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st,
+                        int g_begin = 0, int g_end = -1);   // tile groups [g_begin, g_end) of the mask
 int dltb_norm_bwd_partials(int N);
 void dltb_norm_bwd_dx(const void* dy, const void* s, const void* w, const float* mean,
                       const float* rstd, const void* dres, void* dx, int N, int d, bool rms,

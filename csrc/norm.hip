@@ -136,6 +136,7 @@ struct MaskJob {
   const int64_t* seed;
   int64_t site;
   int gx;              // query chunks of 256 per tile group
+  int g0;              // first tile group of this launch (a mask may be split over two launches)
 };
 
 template <int NV, bool RMS, bool HAS_RES>
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(256) void norm_fwd_mask_kernel(
   } else {
     const int m = bid - nb_norm;
     attn_mask_word(mj.mask, mj.T, mj.thr16, mj.seed, mj.site, (m % mj.gx) * 256 + threadIdx.x,
-                   (uint32_t)(m / mj.gx));
+                   (uint32_t)(mj.g0 + m / mj.gx));
   }
 }
 
@@ -495,11 +496,14 @@ void launch_fwd_mask_t(int nv, int nb_norm, int nb_mask, hipStream_t st, const b
 void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void* b, void* s_out, void* y,
                         float* mean, float* rstd, int N, int d, float eps, bool rms, uint32_t thr16,
                         float drop_scale, const int64_t* seed, int64_t site, uint32_t* mask, int B, int T,
-                        int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st) {
+                        int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st,
+                        int g_begin, int g_end) {
   const int nv = nv_for(d);
-  const MaskJob mj{mask, T, mask_thr16, mask_seed, mask_site, cdiv(T, 256)};
+  const int ng = B * Hq * (T / kMaskKeyTile) * 2;          // tile groups of the whole mask
+  if (g_end < 0 || g_end > ng) g_end = ng;
+  const MaskJob mj{mask, T, mask_thr16, mask_seed, mask_site, cdiv(T, 256), g_begin};
   const int nb_norm = cdiv(N, kWaves);
-  const int nb_mask = mj.gx * B * Hq * (T / kMaskKeyTile) * 2;
+  const int nb_mask = g_end > g_begin ? mj.gx * (g_end - g_begin) : 0;
   auto X = (const bf16_t*)x;
   auto R = (const bf16_t*)r;
   auto W = (const bf16_t*)w;

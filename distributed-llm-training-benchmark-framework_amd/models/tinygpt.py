@@ -22,6 +22,7 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
+import os
 from types import SimpleNamespace
 
 import torch
@@ -115,10 +116,13 @@ class _BlockFn(torch.autograd.Function):
         p = model.drop_p
         lb = model.layer_buffer(i)          # layer-strided GEMM operands (batched weight gradients)
         # LN1 (with the previous block's MLP dropout + residual) and this block's attention-dropout
-        # mask: one launch on the GPU
+        # mask: one launch on the GPU.  With mask_split the previous block's LN2 launch already
+        # generated the first half of this mask (model._next_amask) and LN1 adds the second half.
+        prev, model._next_amask = model._next_amask, None
         x, h1, mean1, rstd1, amask = F_.norm_fwd_mask(
             x_in, m_in, ln1w, ln1b, LN_EPS, False, p if m_in is not None else 0.0, rt.seed,
-            model.site_mlp(i - 1) if m_in is not None else 0, lb and lb.h1, B, T, H, p, model.site_attn(i))
+            model.site_mlp(i - 1) if m_in is not None else 0, lb and lb.h1, B, T, H, p, model.site_attn(i),
+            mask_out=prev, part=1 if prev is not None else None)
         if m_in is None:                    # block 0: the embedding output is the residual stream
             x = x_in
         qkv = F_.linear_fwd(h1, win, bin_)
@@ -126,7 +130,13 @@ class _BlockFn(torch.autograd.Function):
                                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i),
                                     amask, o_out=lb and lb.o)
         a = F_.linear_fwd(o, wo, bo)
-        x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
+        if model.mask_split and p > 0 and i + 1 < cfg.n_layer and x.is_cuda:
+            # LN2 (latency-bound) beside the first half of the NEXT block's attention-dropout mask
+            x1, h2, mean2, rstd2, model._next_amask = F_.norm_fwd_mask(
+                x, a, ln2w, ln2b, LN_EPS, False, 0.0, rt.seed, 0, lb and lb.h2, B, T, H, p,
+                model.site_attn(i + 1), part=0)
+        else:
+            x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
         f = F_.linear_fwd(h2, w1, b1)
         g = F_.gelu_fwd(f, out=lb and lb.g)
         m = F_.linear_fwd(g, w2, b2)        # Dropout(m) + x1 happens in the consumer's LayerNorm
@@ -266,6 +276,10 @@ class TinyGPT(nn.Module):
         self.drop_p = cfg.dropout
         self._lbufs = None
         self._lbuf_key = None
+        # each attention-dropout mask is generated in two halves, beside the previous block's LN2
+        # and beside this block's LN1 (both latency-bound row norms that leave VALU issue idle)
+        self.mask_split = os.environ.get("DLTB_MASK_SPLIT", "1") == "1"
+        self._next_amask = None
         self._build_units()
 
     @staticmethod
@@ -358,6 +372,7 @@ class TinyGPT(nn.Module):
         if self.drop_p > 0 and self.rt.seed is None:
             raise RuntimeError("dropout needs a StepSeed on the runtime (engine.attach or rt.seed = ...)")
         self._lbuf_on = False
+        self._next_amask = None
         self._prepare_layer_buffers(B * T, self.transformer["wte"].weight)
         anchor = torch.empty((), requires_grad=True)    # graph entry (CPU scalar, never updated)
         x = _EmbedFn.apply(anchor, idx, self)

@@ -40,16 +40,23 @@ def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0, y_out=None):
     return s, _into(y_out, y), mean, rstd
 
 
-def norm_fwd_mask(x, r, w, b, eps, rms, p, seed, site, y_out, B, T, Hq, p_attn, attn_site):
+def norm_fwd_mask(x, r, w, b, eps, rms, p, seed, site, y_out, B, T, Hq, p_attn, attn_site, mask_out=None,
+                  part=None):
     """norm_fwd plus the attention-dropout mask of (B, T, Hq) at ``attn_site``, on the GPU in one
     launch (csrc/norm.hip norm_fwd_mask_kernel).  Returns (s, y, mean, rstd, mask); mask is None on
-    the CPU or without attention dropout."""
+    the CPU or without attention dropout.  ``part`` = 0 / 1: only the first / second half of the
+    mask's tile groups, written into ``mask_out`` (or a new mask for part 0) -- a mask generated
+    by two launches, each beside a latency-bound row norm."""
     if _gpu(x) and p_attn > 0:
+        g0, g1 = 0, -1
+        if part is not None:
+            half = (B * Hq * (T // 64) * 2) // 2
+            g0, g1 = (0, half) if part == 0 else (half, -1)
         s_, y, mean, rstd, mask = ext().norm_fwd_mask(x, r, w, b, eps, rms, p, seed.device_tensor, site, y_out,
-                                                      B, T, Hq, p_attn, attn_site)
+                                                      B, T, Hq, p_attn, attn_site, mask_out, g0, g1)
         return (s_ if r is not None else None), y, (None if rms else mean), rstd, mask
     s_, y, mean, rstd = norm_fwd(x, r, w, b, eps, rms, p, seed, site, y_out)
-    return s_, y, mean, rstd, attn_mask(B, T, Hq, p_attn, seed, attn_site, x)
+    return s_, y, mean, rstd, (attn_mask(B, T, Hq, p_attn, seed, attn_site, x) if part is None else None)
 
 
 # colpart segment kinds (csrc/colreduce.hip)

@@ -66,3 +66,28 @@ def test_engine_step_every_strategy(strategy):
     assert losses[-1] < losses[0], losses      # memorising one batch must reduce the loss
     sd = eng.full_state_dict()
     assert sd["transformer.wte.weight"].shape == (cfg.vocab_size, cfg.n_embd)
+
+
+def test_split_mask_generation_is_bitwise_identical():
+    """mask_split: each block's attention-dropout mask is generated in two halves (beside the
+    previous block's LN2 and beside its own LN1).  Loss and every gradient must be bitwise what the
+    single LN1 + mask launch per block gives."""
+    torch.manual_seed(0)
+    cfg = _cfg(T=256, layers=3)
+    ref_m = build_model(cfg).to("cuda", torch.bfloat16)
+    outs = []
+    for on in (False, True):
+        m = copy.deepcopy(ref_m)
+        m.mask_split = on
+        m.rt = ParamRuntime()
+        s = StepSeed(11, device="cuda")
+        s.next()
+        m.rt.seed = s
+        m.train()
+        idx = torch.randint(0, cfg.vocab_size, (2, cfg.block_size), generator=torch.Generator().manual_seed(3))
+        _, loss = m(idx.cuda(), idx.cuda())
+        loss.backward()
+        outs.append((loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for n in outs[0][1]:
+        assert torch.equal(outs[0][1][n], outs[1][1][n]), n
