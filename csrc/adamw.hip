@@ -112,12 +112,24 @@ template <typename G>
 __global__ __launch_bounds__(256) void sumsq_kernel(const G* __restrict__ x, long n4,
                                                    float* __restrict__ part) {
   __shared__ float red[4];
-  float acc = 0.f;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+  // four grid-strided loads issued before any is consumed (four independent accumulators): the
+  // pass is HBM-latency bound with one 8-byte load in flight per lane
+  const long stride = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    float g[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load4<G>(x + (i + u * stride) * 4, g[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += g[u][0] * g[u][0] + g[u][1] * g[u][1] + g[u][2] * g[u][2] + g[u][3] * g[u][3];
+  }
+  for (; i < n4; i += stride) {
     float g[4];
     load4<G>(x + i * 4, g);
-    acc += g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
+    a[0] += g[0] * g[0] + g[1] * g[1] + g[2] * g[2] + g[3] * g[3];
   }
+  float acc = (a[0] + a[1]) + (a[2] + a[3]);
   acc = block_sum(acc, red);
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
