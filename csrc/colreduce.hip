@@ -118,10 +118,26 @@ __global__ __launch_bounds__(256) void colreduce_multi_kernel(ColRedArgs A) {
   const int c0 = blockIdx.x * 64 + cq * 4;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c0 < k) {
-    for (int p = ph; p < S.P; p += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(S.part + (size_t)p * k + c0);
-      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    // four partial rows in flight per lane (independent sums, added in a fixed order)
+    float4 b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int p = ph;
+    for (; p + 48 < S.P; p += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(S.part + (size_t)(p + 16 * u) * k + c0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { b[u].x += v[u].x; b[u].y += v[u].y; b[u].z += v[u].z; b[u].w += v[u].w; }
     }
+    for (; p < S.P; p += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(S.part + (size_t)p * k + c0);
+      b[0].x += v.x; b[0].y += v.y; b[0].z += v.z; b[0].w += v.w;
+    }
+    a.x = (b[0].x + b[1].x) + (b[2].x + b[3].x);
+    a.y = (b[0].y + b[1].y) + (b[2].y + b[3].y);
+    a.z = (b[0].z + b[1].z) + (b[2].z + b[3].z);
+    a.w = (b[0].w + b[1].w) + (b[2].w + b[3].w);
   }
   red[ph][cq * 4 + 0] = a.x;
   red[ph][cq * 4 + 1] = a.y;
