@@ -22,7 +22,6 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
-import os
 from types import SimpleNamespace
 
 import torch
@@ -278,7 +277,7 @@ class TinyGPT(nn.Module):
         self._lbuf_key = None
         # each attention-dropout mask is generated in two halves, beside the previous block's LN2
         # and beside this block's LN1 (both latency-bound row norms that leave VALU issue idle)
-        self.mask_split = os.environ.get("DLTB_MASK_SPLIT", "1") == "1"
+        self.mask_split = True         # (attribute, not an env switch: tests compare both paths)
         self._next_amask = None
         self._build_units()
 
