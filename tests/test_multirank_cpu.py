@@ -11,3 +11,20 @@ def test_world2_equals_world1_cpu(tmp_path):
     assert set(ws1) == set(ws2)
     bad = compare(ws1, ws2, loss_tol=1e-4, upd_tol=1e-3, cos_min=0.99999, param_tol=1e-3)
     assert not bad, bad
+
+
+def test_rccl_equivalence_script_cpu(tmp_path):
+    """The suite's step 0 (scripts/rccl_equivalence.py) end to end on gloo: world 2 vs world 1 for
+    every case, one JSON verdict, exit status 0."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "rq.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "rccl_equivalence.py"), "--ws", "2",
+                        "--device", "cpu", "--out", str(out)], capture_output=True, text=True, env=env, timeout=900)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    v = json.loads(out.read_text())
+    assert v["pass"] and v["world_sizes"]["2"]["mismatches"] == [] and len(v["world_sizes"]["2"]["cases"]) == 8
