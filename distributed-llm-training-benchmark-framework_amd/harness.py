@@ -179,8 +179,12 @@ def train(args):
             if is_main:
                 print(f"Resumed from {args.resume}: optimizer step {meta['opt_steps']}", flush=True)
         engine.train()
+        # (auto: a warm-up no longer than one accumulation window would put the graph capture, at the
+        # first window start after an eager window, inside the timed steps -> eager; as fast)
+        short_warmup = (args.graphs == "auto" and args.warmup_steps <= engine.accum
+                        and os.environ.get("DLTB_GRAPHS") is None)
         runner = GraphedStep(engine) if (graphs_enabled(args.graphs, device, world) and not args.profile
-                                         and not args.phase_timers) else None
+                                         and not args.phase_timers and not short_warmup) else None
         timers = PhaseTimers(device) if args.phase_timers else None
         timed_n = max(0, args.steps - args.warmup_steps)
         # per-step losses are COPIED into a device buffer: a graph replay returns the same static
