@@ -62,10 +62,12 @@ def build_parser():
     ap.add_argument("--grad-reduce", default="micro", choices=["micro", "window"],
                     help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed stage 2, default) or "
                          "once per accumulation window (ZeRO-1 communication, reported as zero1-dpN)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"],
-                    help="compute dtype (fp16: dynamic loss scaling, the reference's DDP/FSDP precision)")
-    ap.add_argument("--grad-comm-dtype", default="compute", choices=["compute", "fp32"],
-                    help="DDP gradient all-reduce dtype (fp32 = the reference's torch DDP)")
+    ap.add_argument("--dtype", default="auto", choices=["auto", "bf16", "fp16"],
+                    help="compute dtype; auto = the reference's precision per strategy (as the harness): bf16 "
+                         "for ZeRO-2/3 (zero2.json), fp16 + dynamic loss scaling for DDP/FSDP (autocast)")
+    ap.add_argument("--grad-comm-dtype", default="auto", choices=["auto", "compute", "fp32"],
+                    help="DDP gradient all-reduce dtype; auto = fp32 for fp16 DDP (the reference's torch DDP "
+                         "reduces fp32 grads), else the compute dtype")
     ap.add_argument("--fsdp-wrap", default="block", choices=["block", "root"],
                     help="FSDP unit layout: per transformer block, or the reference's single root FlatParameter")
     ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
@@ -106,6 +108,15 @@ def launch(args, argv) -> int:
     return proc.returncode
 
 
+def resolve_precision(args):
+    """--dtype / --grad-comm-dtype auto -> the reference's precision per strategy (harness.py)."""
+    if args.dtype == "auto":
+        args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
+    if args.grad_comm_dtype == "auto":
+        args.grad_comm_dtype = "fp32" if (args.strategy == "ddp" and args.dtype == "fp16") else "compute"
+    return args
+
+
 def run_rank(args) -> int:
     import torch
     import dltb  # noqa: F401
@@ -117,6 +128,7 @@ def run_rank(args) -> int:
     from dltb.utils.dist import all_reduce_max, barrier, cleanup_distributed, setup_distributed
     from dltb.utils.timers import PhaseTimers
 
+    resolve_precision(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -212,6 +224,7 @@ def run_rank(args) -> int:
         if rank == 0:
             flops = mcfg.train_flops_per_token(args.seq_len)
             same = BASELINES.get(args.strategy) if label == args.strategy else None
+            ref_dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
             out = {
                 "metric": "tokens_per_sec",
                 "value": value,
@@ -254,6 +267,8 @@ def run_rank(args) -> int:
                                  "vs_baseline_per_gpu = (value / n_gpus) / (18147 / 4), the per-GPU ratio",
                 "vs_baseline_per_gpu": (value / world) / (BASELINE_TPS / 4) if (args.tier == "A" and args.seq_len == 2048) else None,
                 "same_strategy_published": same,
+                "same_strategy_precision_matches": (args.dtype == ref_dtype) if same else None,
+                "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
                 "gemm_tuning": tmode,
                 "hip_graphs": graphed,
             }

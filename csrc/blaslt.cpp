@@ -11,6 +11,7 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <algorithm>
+#include <list>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -34,13 +35,16 @@ hipblasLtHandle_t handle() {
   return h;
 }
 
-void* workspace() {
-  static void* ws = [] {
-    void* p = nullptr;
-    if (hipMalloc(&p, kWorkspace) != hipSuccess) throw std::runtime_error("blaslt workspace alloc failed");
-    return p;
-  }();
-  return ws;
+// One split-K workspace per stream: two tuned split-K GEMMs running concurrently on different
+// streams must not share their partials buffer.
+void* workspace(hipStream_t st) {
+  static std::map<hipStream_t, void*> ws;
+  auto it = ws.find(st);
+  if (it != ws.end()) return it->second;
+  void* p = nullptr;
+  if (hipMalloc(&p, kWorkspace) != hipSuccess) throw std::runtime_error("blaslt workspace alloc failed");
+  ws.emplace(st, p);
+  return p;
 }
 
 hipblasOperation_t op(int t) { return t ? HIPBLAS_OP_T : HIPBLAS_OP_N; }
@@ -100,7 +104,7 @@ float time_one(hipblaslt_ext::Gemm& g, hipblasLtMatmulAlgo_t algo, int splitk, i
   auto t = tuning_of(splitk, wgm);
   size_t need = 0;
   if (g.isAlgoSupported(algo, t, need) != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) return -1.f;
-  if (g.initialize(algo, t, workspace(), true, st) != HIPBLAS_STATUS_SUCCESS) return -1.f;
+  if (g.initialize(algo, t, workspace(st), true, st) != HIPBLAS_STATUS_SUCCESS) return -1.f;
   for (int i = 0; i < 2; ++i)
     if (g.run(st) != HIPBLAS_STATUS_SUCCESS) return -1.f;
   hipEventRecord(e0, st);
@@ -112,21 +116,28 @@ float time_one(hipblaslt_ext::Gemm& g, hipblasLtMatmulAlgo_t algo, int splitk, i
   return ms * 1000.f / iters;
 }
 
-// Initialised problems keyed by shape, tuning AND operand pointers: the model's GEMM operands live
-// in preallocated (layer-strided) buffers, so every call site repeats its pointers step after step
-// and, after the first step, is a bare kernel launch (also inside HIP-graph capture).
+// Initialised problems keyed by shape, tuning, stream AND operand pointers: the model's GEMM
+// operands live in preallocated (layer-strided) buffers, so every call site repeats its pointers
+// step after step and, after the first step, is a bare kernel launch (also inside HIP-graph
+// capture).  Least-recently-used entries are evicted one at a time, so pointers churned by the
+// caching allocator (eager multi-rank runs) never flush the hot call sites.
 using Key = std::tuple<int, int, long, long, long, long, long, long, long, long, long, long, int, int, int, int, int,
-                       int, const void*, const void*, const void*, const void*>;
+                       int, const void*, const void*, const void*, const void*, const void*>;
 constexpr size_t kMaxCached = 8192;
 
 Key key_of(const BltProblem& p, int algo, int splitk, int wgm, const void* A, const void* B, const void* C,
-           const void* bias) {
+           const void* bias, hipStream_t st) {
   return Key{p.opA, p.opB, p.m, p.n, p.k, p.batch, p.lda, p.ldb, p.ldc, p.sa, p.sb, p.sc, p.f16, p.beta1,
-             p.bias, algo, splitk, wgm, A, B, C, bias};
+             p.bias, algo, splitk, wgm, A, B, C, bias, (const void*)st};
 }
 
-std::map<Key, std::unique_ptr<hipblaslt_ext::Gemm>>& cache() {
-  static std::map<Key, std::unique_ptr<hipblaslt_ext::Gemm>> c;
+struct Lru {
+  std::list<Key> order;     // most recently used first
+  std::map<Key, std::pair<std::unique_ptr<hipblaslt_ext::Gemm>, std::list<Key>::iterator>> map;
+};
+
+Lru& cache() {
+  static Lru c;
   return c;
 }
 
@@ -175,9 +186,9 @@ int dltb_blaslt_run(const BltProblem& p, const void* A, const void* B, void* C, 
                     int splitk, int wgm, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_mu);
   auto& c = cache();
-  const Key key = key_of(p, algo, splitk, wgm, A, B, C, bias);
-  auto it = c.find(key);
-  if (it == c.end()) {
+  const Key key = key_of(p, algo, splitk, wgm, A, B, C, bias, st);
+  auto it = c.map.find(key);
+  if (it == c.map.end()) {
     hipblasLtMatmulAlgo_t a;
     if (!algo_of(algo, a)) return -1;
     auto g = make_gemm(p, A, B, C, bias);
@@ -185,11 +196,17 @@ int dltb_blaslt_run(const BltProblem& p, const void* A, const void* B, void* C, 
     auto t = tuning_of(splitk, wgm);
     size_t need = 0;
     if (g->isAlgoSupported(a, t, need) != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) return -3;
-    if (g->initialize(a, t, workspace(), true, st) != HIPBLAS_STATUS_SUCCESS) return -4;
-    if (c.size() >= kMaxCached) c.clear();    // transient (allocator-churned) pointers: start over
-    it = c.emplace(key, std::move(g)).first;
+    if (g->initialize(a, t, workspace(st), true, st) != HIPBLAS_STATUS_SUCCESS) return -4;
+    if (c.map.size() >= kMaxCached) {       // evict the least recently used problem
+      c.map.erase(c.order.back());
+      c.order.pop_back();
+    }
+    c.order.push_front(key);
+    it = c.map.emplace(key, std::make_pair(std::move(g), c.order.begin())).first;
+  } else if (it->second.second != c.order.begin()) {
+    c.order.splice(c.order.begin(), c.order, it->second.second);
   }
-  return it->second->run(st) == HIPBLAS_STATUS_SUCCESS ? 0 : -5;
+  return it->second.first->run(st) == HIPBLAS_STATUS_SUCCESS ? 0 : -5;
 }
 
 std::string dltb_blaslt_name(int algo) {

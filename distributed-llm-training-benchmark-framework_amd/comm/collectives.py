@@ -23,6 +23,17 @@ engines own their communication, and this module is the one place that talks to
   per-bucket batched weight gradients, deferred all-gathers waited in ``acquire``, fp32
   accumulation of reduce-scattered chunks, ZeRO-3 transient gather buffers) runs with the real
   HIP kernels.  It is a correctness mode, not a performance mode.
+* Emulated fabric (``DLTB_COMM=emulate:N``, one process, one GPU): ``world = N`` and ``rank =
+  $DLTB_EMU_RANK`` (default 0) with NO process group, so the engines build the real N-rank layouts,
+  shards, bucket plans, tail-deferral and per-rank memory footprint.  Each collective runs, on a
+  high-priority side stream with RCCL's event semantics (the caller's stream waits only at
+  ``wait()``), ONE paced kernel (csrc/comm_emu.hip) that keeps ``$DLTB_EMU_CHANNELS`` (32)
+  workgroups resident for the alpha-beta-modelled duration of that collective at N ranks
+  (comm/topology.py), reads its buffer through HBM and writes a local stand-in for its result
+  (reduce-scatter: N x the own chunk; all-reduce: x N; all-gather into a fresh buffer: the own
+  shard replicated; in place: unchanged).  The step time it produces is a PREDICTION of the N-GPU
+  step -- overlap, exposed communication and the CU/HBM contention of the collectives are real,
+  the fabric itself is the model.  On the CPU only the numerics run (wire-byte accounting tests).
 * Lazy mode (``DLTB_COMM_LAZY=1``, tests): an asynchronous collective runs only when its work is
   waited -- it reads its input and writes its output at ``wait()``, the latest moment RCCL could.
   A rank that overwrites a buffer still being reduced, reads a result before waiting for it, or
@@ -35,6 +46,38 @@ from collections import OrderedDict
 
 import torch
 import torch.distributed as dist
+
+
+class _EmuWork:
+    """Emulated collective in flight on the emulation stream (an event the caller's stream waits
+    for at ``wait()``, like a ProcessGroupNCCL work)."""
+
+    def __init__(self, ev, keep):
+        self._ev = ev
+        self._keep = keep            # tensors the side stream still uses
+
+    def wait(self):
+        if self._ev is not None:
+            torch.cuda.current_stream().wait_event(self._ev)
+            self._keep = None
+        return True
+
+    def is_completed(self):
+        return self._ev is None or self._ev.query()
+
+
+def emulated_world():
+    """N of ``DLTB_COMM=emulate:N`` (0 when not emulating)."""
+    mode = os.environ.get("DLTB_COMM", "")
+    if not mode.startswith("emulate"):
+        return 0
+    try:
+        n = int(mode.split(":", 1)[1])
+    except (IndexError, ValueError):
+        raise ValueError(f"DLTB_COMM={mode!r}: expected emulate:N") from None
+    if n < 1:
+        raise ValueError("DLTB_COMM=emulate:N needs N >= 1")
+    return n
 
 
 class _Done:
@@ -51,15 +94,28 @@ _DONE = _Done()
 
 
 class _Lazy:
-    """Work whose collective runs at the first ``wait()`` (lazy mode)."""
+    """Work whose collective runs at the first ``wait()`` (lazy mode).  Collectives still run in
+    the order they were issued, as on RCCL's stream: waiting for one first runs every earlier
+    collective of the same comm still queued (ranks may wait in different orders -- a rank whose
+    unit did not report drains its buckets elsewhere -- but they issue in the same order)."""
 
-    def __init__(self, fn):
+    def __init__(self, fn, queue):
         self._fn = fn
+        self._queue = queue
+        queue.append(self)
 
-    def wait(self):
+    def _run(self):
         if self._fn is not None:
             fn, self._fn = self._fn, None
             fn()
+
+    def wait(self):
+        if self._fn is not None:
+            while self._queue:
+                w = self._queue.pop(0)
+                w._run()
+                if w is self:
+                    break
         return True
 
     def is_completed(self):
@@ -80,13 +136,29 @@ def ring_factor(op: str, world: int) -> float:
 class Comm:
     def __init__(self, group=None):
         self.group = group
-        self.enabled = dist.is_available() and dist.is_initialized()
+        self.emulate = emulated_world()
+        self.enabled = dist.is_available() and dist.is_initialized() and not self.emulate
         self.world = dist.get_world_size(group) if self.enabled else 1
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.backend = dist.get_backend(group) if self.enabled else "none"
+        if self.emulate:
+            self.world, self.rank, self.backend = self.emulate, int(os.environ.get("DLTB_EMU_RANK", "0")), "emulate"
+            if not 0 <= self.rank < self.world:
+                raise ValueError(f"DLTB_EMU_RANK={self.rank} outside emulate:{self.world}")
+            from .topology import measured_params
+            self.emu_channels = int(os.environ.get("DLTB_EMU_CHANNELS", "32"))
+            self.emu_passes = int(os.environ.get("DLTB_EMU_HBM_PASSES", "1"))
+            self.emu_params = {}          # op -> (alpha_us, bus_GBps, source)
+            for op in ("all_reduce", "reduce_scatter", "all_gather", "broadcast", "all_to_all"):
+                a, b, src = measured_params(self.world, "all_reduce" if op == "all_reduce" else "reduce_scatter")
+                a = float(os.environ.get("DLTB_EMU_ALPHA_US", a))
+                b = float(os.environ.get("DLTB_EMU_BUS_GBPS", b))
+                self.emu_params[op] = (a, b, src)
+            self._emu_stream = None
         self.staged = self.backend == "gloo"      # device tensors go through host memory
-        self.lazy = os.environ.get("DLTB_COMM_LAZY", "0") == "1"
+        self.lazy = os.environ.get("DLTB_COMM_LAZY", "0") == "1" and not self.emulate
         self._pending = []
+        self._lazy_queue = []                 # lazy mode: issued, not yet run (issue order)
         self.stats = OrderedDict()            # op -> {"calls": n, "wire_bytes": b}
 
     # ------------------------------------------------------------------ accounting
@@ -94,6 +166,14 @@ class Comm:
         s = self.stats.setdefault(op, {"calls": 0, "wire_bytes": 0})
         s["calls"] += 1
         s["wire_bytes"] += int(t.numel() * t.element_size() * ring_factor(op, self.world))
+        if self.emulate:
+            a, b = self._emu_time(op, t)
+            s["model_us"] = s.get("model_us", 0.0) + a + b
+
+    def modelled_us(self) -> float:
+        """Emulated fabric: the summed alpha-beta time of every collective issued since the last
+        ``reset_stats`` (what the fabric would be busy for, overlapped or not)."""
+        return sum(s.get("model_us", 0.0) for s in self.stats.values())
 
     def wire_bytes(self) -> int:
         return sum(s["wire_bytes"] for s in self.stats.values())
@@ -128,12 +208,62 @@ class Comm:
         if dst.data_ptr() != h.data_ptr() or dst.device != h.device:
             dst.copy_(h)
 
+    # ------------------------------------------------------------------ emulated fabric
+    def _emu_time(self, op, full):
+        """(alpha_us, beta_us) of ``op`` on the full buffer ``full`` at ``self.world`` ranks."""
+        a, bus, _ = self.emu_params["all_to_all" if op == "all_to_all" else op]
+        nbytes = full.numel() * full.element_size()
+        return a, nbytes * ring_factor(op, self.world) / (bus * 1e3)
+
+    def _emu(self, op, full, dst=None, src=None, scale=1.0, replicas=1, rep_stride=0,
+             async_op=True, track=True):
+        """One emulated collective: numerics stand-in ``dst[r*rep_stride + j] = scale * src[j]``
+        plus, on a GPU, the paced kernel on the emulation stream."""
+        if not full.is_cuda:
+            if src is not None:
+                v = src * scale if scale != 1.0 else src
+                for r in range(replicas):
+                    dst.view(-1)[r * rep_stride:r * rep_stride + src.numel()].copy_(v.view(-1))
+            return _DONE
+        from ..ops._ext import ext
+        if self._emu_stream is None:
+            self._emu_stream = torch.cuda.Stream(device=full.device, priority=-1)
+        side, cur = self._emu_stream, torch.cuda.current_stream(full.device)
+        side.wait_stream(cur)                 # the collective starts after its producers
+        alpha, beta = self._emu_time(op, full)
+        with torch.cuda.stream(side):
+            ext().comm_emu(full, self.emu_passes, dst, src, float(scale), int(replicas), int(rep_stride),
+                           float(alpha), float(beta), self.emu_channels)
+        keep = [t for t in (full, dst, src) if t is not None]
+        for t in keep:
+            t.record_stream(side)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        w = _EmuWork(ev, keep)
+        if not async_op:
+            w.wait()
+            return _DONE
+        return self._track(w, True) if track else w
+
+    def _emu_gather(self, out, inp, async_op, track):
+        n = inp.numel()
+        off = out.data_ptr() + self.rank * n * out.element_size()
+        if inp.data_ptr() == off and inp.dtype == out.dtype:     # in place: the own chunk is already there
+            return self._emu("all_gather", out, async_op=async_op, track=track)
+        return self._emu("all_gather", out, out.view(-1), inp.reshape(-1), 1.0, self.world, n,
+                         async_op=async_op, track=track)
+
     # ------------------------------------------------------------------ collectives
+    def _flush_lazy(self):
+        while self._lazy_queue:                   # earlier collectives complete first
+            self._lazy_queue.pop(0)._run()
+
     def _lazy(self, fn, async_op: bool, track: bool):
         if not async_op:
+            self._flush_lazy()
             fn()
             return _DONE
-        w = _Lazy(fn)
+        w = _Lazy(fn, self._lazy_queue)
         return self._track(w, True) if track else w
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum", async_op: bool = True, track: bool = True):
@@ -141,6 +271,9 @@ class Comm:
         if self.world == 1:
             return _DONE
         self._count("all_reduce", t)
+        if self.emulate:
+            sc = float(self.world) if op == "sum" else 1.0
+            return self._emu("all_reduce", t, t.view(-1), t.view(-1), sc, async_op=async_op, track=track)
         if self.lazy:
             return self._lazy(lambda: self._all_reduce(t, op), async_op, track)
         return self._all_reduce(t, op, async_op, track)
@@ -164,6 +297,11 @@ class Comm:
             return _DONE
         assert inp.numel() == out.numel() * self.world, "reduce_scatter: input must be world x output"
         self._count("reduce_scatter", inp)
+        if self.emulate:
+            n = out.numel()
+            mine = inp.reshape(-1)[self.rank * n:(self.rank + 1) * n]
+            return self._emu("reduce_scatter", inp, out.view(-1), mine, float(self.world),
+                             async_op=async_op, track=track)
         if self.lazy:
             return self._lazy(lambda: self._reduce_scatter(out, inp), async_op, track)
         return self._reduce_scatter(out, inp, async_op, track)
@@ -187,6 +325,8 @@ class Comm:
             return _DONE
         assert out.numel() == inp.numel() * self.world, "all_gather: output must be world x input"
         self._count("all_gather", out)
+        if self.emulate:
+            return self._emu_gather(out, inp, async_op, track)
         if self.lazy:
             return self._lazy(lambda: self._all_gather(out, inp), async_op, track)
         return self._all_gather(out, inp, async_op, track)
@@ -203,7 +343,11 @@ class Comm:
     def broadcast(self, t: torch.Tensor, src: int = 0):
         if self.world == 1:
             return
+        self._flush_lazy()
         self._count("broadcast", t)
+        if self.emulate:
+            self._emu("broadcast", t, async_op=False)
+            return
         if self.staged and t.is_cuda:
             h = self._host(t)
             dist.broadcast(h, src=src, group=self.group)
@@ -215,7 +359,10 @@ class Comm:
         if self.world == 1:
             out.copy_(inp)
             return _DONE
+        self._flush_lazy()
         self._count("all_to_all", inp)
+        if self.emulate:
+            return self._emu("all_to_all", inp, out.view(-1), inp.reshape(-1), async_op=async_op)
         if self.staged and (inp.is_cuda or out.is_cuda):
             h = torch.empty(out.shape, dtype=out.dtype)
             dist.all_to_all_single(h, self._host(inp), group=self.group)
@@ -225,13 +372,15 @@ class Comm:
         return self._track(w, async_op)
 
     def barrier(self):
-        if self.world > 1:
+        if self.world > 1 and not self.emulate:
+            self._flush_lazy()
             dist.barrier(group=self.group)
 
     def max_scalar(self, x: float, device) -> float:
         """Host float max over ranks (timings, peak memory)."""
-        if self.world == 1:
+        if self.world == 1 or self.emulate:
             return x
+        self._flush_lazy()
         t = torch.tensor([x], dtype=torch.float64, device="cpu" if self.staged else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())

@@ -81,6 +81,7 @@ class Engine(ParamRuntime):
         self._gscale = torch.ones(1, device=self.device, dtype=torch.float32)
         self.comm_bytes_per_step = 0
         self.timers = None               # utils.timers.PhaseTimers while the harness times phases
+        self._reported = set()   # id(unit) of the units whose backward reported this micro-step
         self._cache_wt = False   # subclasses: True where parameters stay resident between steps
         self._wt = {}            # (unit index, param index) -> (W view, W^T view of a stacked buffer)
         self._wt_stack = {}      # (param index, shape) -> [units, K, N] buffer of transposes
@@ -263,6 +264,28 @@ class Engine(ParamRuntime):
         acc = self._written.get(key, False)
         self._written[key] = True
         return acc
+
+    def _zero_unreported(self):
+        """Units whose backward did not run this micro-step (parameters the loss does not use: torch
+        DDP's ``find_unused_parameters`` case, which the reference turns off, train_harness.py:221):
+        every gradient slot of theirs that holds nothing of the current accumulation window is
+        zeroed (and marked written), so a stale gradient of an earlier step is never reduced or
+        applied.  Returns those units."""
+        units = self.model.units()
+        if len(self._reported) >= len(units):
+            self._reported.clear()
+            return []
+        out = []
+        for u in units:
+            if id(u) in self._reported:
+                continue
+            for i in range(len(u.params)):
+                t, acc = self.grad_slot(u, i)
+                if not acc:
+                    t.zero_()
+            out.append(u)
+        self._reported.clear()
+        return out
 
     # ------------------------------------------------------------------ helpers
     def _wait_works(self):

@@ -18,7 +18,8 @@ DeepSpeed ZeRO-2), re-built on ``torch.distributed`` (RCCL over xGMI on MI355X):
   (one float all-reduce), clipping coefficient on device, fused AdamW on the owner shard writing
   the bf16 chunk in place, then an in-place all-gather per bucket re-replicates the parameters.
 * ZeRO-1: like ZeRO-2 but gradients accumulate unsharded and are reduce-scattered at the boundary.
-  This is also ZeRO-2 with ``--grad-reduce window`` (bench.py's default on N > 1).  xGMI links are
+  This is also ZeRO-2 with ``--grad-reduce window`` (reported as ``zero1``; bench.py's default is
+  the per-micro-step ZeRO-2 reduction at every world size).  xGMI links are
   point-to-point, so a ring reduce-scatter is per-link bound, and one reduce-scatter per window
   moves 1/grad_accum of the per-micro-step traffic.  The flat gradient buffer is full-size in both
   modes, so HBM use is the same.  Micro-steps without a collective leave every dW product queued
@@ -131,7 +132,10 @@ class ReplicatedEngine(Engine):
         # instead of one launch per block, and the QKV-bias partials of block i ride along with
         # block i-1's dropout colpart launch instead of a launch of their own
         self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda") else None
-        self._launched = [False] * len(L.buckets)
+        # buckets are reduced strictly in bucket order (torch DDP's Reducer does the same): every
+        # rank must issue its collectives in one sequence, and a unit that does not report on some
+        # rank (an unused parameter) would otherwise reorder that rank's sequence
+        self._next = 0
         # ZeRO-2 per-micro-step reduce-scatter, world > 1: a micro-step that does not end its window
         # leaves its buckets' reduce-scatters in flight instead of waiting at the end of backward; the
         # next backward waits for bucket b (and folds its chunk into the fp32 accumulator) only when it
@@ -195,17 +199,23 @@ class ReplicatedEngine(Engine):
         return self._red
 
     def grads_ready(self, unit):
+        self._reported.add(id(unit))
         b = self._bucket_of.get(id(unit))
         if b is None:
             return
         self._pending[b] -= 1
         if self._pending[b] == 0 and self._reduce_now():
-            self._wq.flush(self.layout.buckets[b].units)        # this bucket's dW, then its collective
-            self._launch(b)
+            while self._next < len(self._pending) and self._pending[self._next] == 0:
+                nb = self._next
+                self._wq.flush(self.layout.buckets[nb].units)   # this bucket's dW, then its collective
+                self._launch(nb)
+                self._next += 1
         # (micro-steps without a collective -- inside a ZeRO-1 / window-reduced accumulation
         # window -- leave every dW queued for the single batched flush at the end of the backward)
 
     def _launch(self, b):
+        if b in self._rs_inflight:
+            self._drain_bucket(b)     # the previous micro-step's reduce-scatter of this bucket
         bk = self.layout.buckets[b]
         g = self.flat_grad[bk.start:bk.end]
         if self.stage == 0:
@@ -223,7 +233,6 @@ class ReplicatedEngine(Engine):
             self._rs_inflight[b] = (w, self._window_pos == 0)
         else:
             self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g)
-        self._launched[b] = True
 
     def _drain_bucket(self, b):
         """Wait for bucket ``b``'s reduce-scatter and add its chunk into the fp32 accumulator."""
@@ -252,17 +261,17 @@ class ReplicatedEngine(Engine):
         if self._red is not None:
             self._red.flush()
         self._wq.flush()                                        # world 1: every block in one batch
+        self._zero_unreported()
         if self._reduce_now():
-            for b, done in enumerate(self._launched):   # units that never reported (unused params)
-                if not done:
-                    self._launch(b)
+            for b in range(self._next, len(self._pending)):   # buckets holding units that never reported
+                self._launch(b)
         self._phase("comm_wait_begin")
         self._wait_works()
         if self._tail_defer and self._is_boundary:
             self._drain_all()                   # the optimizer reads the window's full sum next
         self._phase("comm_wait_end")
         self._pending = [len(b.units) for b in self.layout.buckets]
-        self._launched = [False] * len(self.layout.buckets)
+        self._next = 0
         if self.stage == 2 and self.acc is not None and not self._tail_defer:
             src = self.rs_out if self.world > 1 else self.flat_grad
             first = self._window_pos == 0

@@ -244,7 +244,8 @@ class ShardedEngine(Engine):
     def acquire(self, unit):
         g = self._group_of[id(unit)]
         self._ensure(g)
-        self._prefetch(g, +1)
+        if self.cfg.extra.get("forward_prefetch", True):
+            self._prefetch(g, +1)
         return self._views(unit)
 
     def release_forward(self, unit):
@@ -298,6 +299,7 @@ class ShardedEngine(Engine):
             super().wgrad(unit, i, dy, x, dw, accumulate)
 
     def grads_ready(self, unit):
+        self._reported.add(id(unit))
         g = self._group_of[id(unit)]
         if any(self._persistent(unit, i) for i in range(len(unit.params))):
             self._p_left -= 1
@@ -343,10 +345,12 @@ class ShardedEngine(Engine):
 
     def _finish_backward(self):
         self._wq.flush()
-        if self._p_left != self._p_pending:      # persistent params of units that never reported
-            if self._p_left > 0 or self.world == 1:
-                self._reduce_persistent()
-            self._p_left = self._p_pending
+        self._zero_unreported()                   # slots of units that never reported: zero
+        # persistent parameters: world 1 hands p_grad to the owner space here; world > 1 reduces it
+        # here unless the last unit holding some already did (grads_ready)
+        if self.p_layout.owner_numel and (self.world == 1 or self._p_left > 0):
+            self._reduce_persistent()
+        self._p_left = self._p_pending
         for g in self.groups:                     # groups whose backward did not run fully
             self._reduce_group(g)
             g.bwd_left = len(g.units)

@@ -112,9 +112,12 @@ def engine_config(strategy: str, grad_accum: int = 1, semantics: str = "referenc
         cfg.wrap = "root" if pol in ("size_based", "root", "none") else "block"
         bp = str(fc.get("backward_prefetch", "backward_pre")).lower()
         cfg.prefetch = 0 if bp in ("none", "false", "no") else 1
+        # forward_prefetch (fsdp_config.yaml:9): gather unit i+1 while unit i computes.  False (torch's
+        # default, fsdp_reference_root.yaml) issues each unit's all-gather only when it is needed
+        cfg.extra["forward_prefetch"] = bool(fc.get("forward_prefetch", True)) and cfg.prefetch > 0
         if fc.get("mixed_precision") is False and fc.get("param_dtype") == "float32":
             cfg.compute_dtype = torch.float32
-    if compute_dtype == torch.float16:
+    if cfg.compute_dtype == torch.float16:
         cfg.extra["loss_scaling"] = True     # GradScaler semantics (train_harness.py:334-335, 371-376)
     cfg.extra["semantics"] = semantics
     for k, v in (overrides or {}).items():
