@@ -68,6 +68,8 @@ def build_parser():
     ap.add_argument("--grad-comm-dtype", default="auto", choices=["auto", "compute", "fp32"],
                     help="DDP gradient all-reduce dtype; auto = fp32 for fp16 DDP (the reference's torch DDP "
                          "reduces fp32 grads), else the compute dtype")
+    ap.add_argument("--deepspeed-config", default=None,
+                    help="DeepSpeed JSON for zero2/zero3 (default configs/deepspeed/<strategy>.json)")
     ap.add_argument("--fsdp-wrap", default="block", choices=["block", "root"],
                     help="FSDP unit layout: per transformer block, or the reference's single root FlatParameter")
     ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
@@ -78,6 +80,13 @@ def build_parser():
                     help="cpu = gloo / CPU reference ops (tests of the launcher and the engines)")
     ap.add_argument("--timeout-min", type=int, default=10, help="collective timeout")
     ap.add_argument("--fail-rank", type=int, default=None, help="(tests) this rank raises before timing")
+    ap.add_argument("--emulate", type=int, default=0, metavar="N",
+                    help="PREDICTION mode: one process on one GPU plays rank 0 of an N-rank job -- real N-rank "
+                         "layouts, shards and buckets, every collective an alpha-beta-paced kernel on a "
+                         "side stream (DLTB_COMM=emulate:N, comm/collectives.py); value = N x this rank's tok/s")
+    ap.add_argument("--host-check", action="store_true",
+                    help="after the timed steps: host enqueue time per step while the GPU is held busy "
+                         "(is the eager step host-bound?)")
     return ap
 
 
@@ -134,6 +143,10 @@ def run_rank(args) -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.emulate:
+        if world != 1:
+            raise SystemExit("--emulate runs in ONE process (it plays rank 0 of the N-rank job)")
+        os.environ["DLTB_COMM"] = f"emulate:{args.emulate}"
     device = setup_distributed(world, rank, local, device_type=args.device, timeout_min=args.timeout_min)
     cuda = device.type == "cuda"
     try:
@@ -147,18 +160,19 @@ def run_rank(args) -> int:
         mcfg = get_model_config(args.tier, args.seq_len)
         with torch.device(device):          # random init straight into HBM
             model = build_model(mcfg)
-        bucket_mb = args.bucket_mb if args.bucket_mb is not None else recommend_bucket_mb(world)
-        h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None,
+        eworld = args.emulate or world     # the job's rank count (emulated or real)
+        bucket_mb = args.bucket_mb if args.bucket_mb is not None else recommend_bucket_mb(eworld)
+        h = argparse.Namespace(strategy=args.strategy, deepspeed_config=args.deepspeed_config, fsdp_config=None,
                                grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype=args.dtype,
                                bucket_mb=bucket_mb, seed=42, grad_reduce=args.grad_reduce,
                                grad_comm_dtype=args.grad_comm_dtype,
                                fsdp_wrap=args.fsdp_wrap)
         engine, ecfg = _engine_for(h, model, device)
         ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
-        batches = make_batcher("device", ds, args.per_device_batch, world, rank, args.strategy, device)
+        batches = make_batcher("device", ds, args.per_device_batch, eworld, engine.comm.rank, args.strategy, device)
         engine.train()
         accum = engine.accum
-        use_graphs = graphs_enabled(args.graphs, device, world)
+        use_graphs = graphs_enabled(args.graphs, device, eworld)
         if use_graphs and args.graphs == "auto" and args.warmup <= accum and os.environ.get("DLTB_GRAPHS") is None:
             # the graphs are captured at the first window start after one eager window (micro-step
             # accum + 1); with a shorter warm-up that capture would land inside the timed steps, so
@@ -203,7 +217,12 @@ def run_rank(args) -> int:
         barrier()
         sync()
         elapsed = all_reduce_max(time.perf_counter() - t0, device)
+        wire_timed = engine.comm.wire_bytes()      # the timed steps' collectives (before finalize)
         opt_steps = engine.opt_steps - opt0
+        comm_model_ms = engine.comm.modelled_us() / 1e3 / max(1, args.steps) if args.emulate else None
+        host_ms = None
+        if args.host_check and cuda:
+            host_ms = host_enqueue_ms(one_step, min(args.steps, 6), device)
         engine.finalize()                    # a deferred update of the last window: outside the timed region
         mean_loss = float(loss_hist[:args.steps].mean().item()) if args.steps else 0.0
         final_loss = float(loss.item())
@@ -212,9 +231,9 @@ def run_rank(args) -> int:
         phases = timers.summary() if timers is not None else None
         comm_wait = all_reduce_max(phases["comm_wait"], device) if phases else 0.0
         graphed = bool(runner is not None and runner.graphs and not runner.disabled)
-        wire = engine.comm.wire_bytes() / args.steps if (args.steps and not graphed) else None
+        wire = wire_timed / args.steps if (args.steps and not graphed) else None
         ms = elapsed / max(1, args.steps) * 1e3
-        tokens = args.per_device_batch * args.seq_len * world * args.steps
+        tokens = args.per_device_batch * args.seq_len * eworld * args.steps
         value = tokens / elapsed if elapsed > 0 else 0.0
         label = args.strategy
         if args.strategy == "zero2" and ecfg.zero_stage == 1:
@@ -222,6 +241,7 @@ def run_rank(args) -> int:
         if args.strategy == "fsdp" and ecfg.wrap == "root":
             label = "fsdp_root"
         if rank == 0:
+            world = eworld if args.emulate else world
             flops = mcfg.train_flops_per_token(args.seq_len)
             same = BASELINES.get(args.strategy) if label == args.strategy else None
             ref_dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
@@ -272,6 +292,26 @@ def run_rank(args) -> int:
                 "gemm_tuning": tmode,
                 "hip_graphs": graphed,
             }
+            if args.emulate:
+                out.update({
+                    "metric": "tokens_per_sec_predicted",
+                    "n_gpus": 1, "emulated_world": eworld, "prediction": True,
+                    "prediction_note": (f"ONE MI355X playing rank {engine.comm.rank} of a {eworld}-rank job: real "
+                                        f"{eworld}-rank layouts / shards / buckets, collectives replaced by alpha-beta "
+                                        "paced kernels on a high-priority side stream (DLTB_COMM=emulate:N); "
+                                        "value = N x this rank's tokens/s; NOT a measurement of N GPUs"),
+                    "comm_model": {op: {"alpha_us": a, "bus_GBps": b, "source": src}
+                                   for op, (a, b, src) in engine.comm.emu_params.items()
+                                   if op in ("all_reduce", "reduce_scatter", "all_gather")},
+                    "emu_channels": engine.comm.emu_channels,
+                    "comm_model_ms_per_step": comm_model_ms,
+                    "vs_baseline": None, "vs_baseline_per_gpu": None,
+                    "predicted_ms_per_step": ms,
+                    "peak_hbm_gb_per_rank": peak_gb,
+                })
+            if host_ms is not None:
+                out["host_enqueue_ms_per_step"] = host_ms
+                out["host_over_gpu"] = host_ms / ms if ms else None
             print(json.dumps(out), flush=True)
         if cuda:
             from dltb.utils.gemm_tuning import flush_tunableop
@@ -279,6 +319,26 @@ def run_rank(args) -> int:
         return 0
     finally:
         cleanup_distributed()
+
+
+def host_enqueue_ms(one_step, k, device):
+    """Host time to enqueue ``k`` eager micro-steps while the GPU is held busy by one long wait
+    kernel in front of them (so no launch waits for the GPU): the host cost per step.  A step that
+    synchronises with the GPU would show as ~the hold time."""
+    import torch
+    from dltb.ops._ext import ext
+    torch.cuda.synchronize(device)
+    hold_us = 3e5 + 5e4 * k
+    ext().comm_emu(None, 1, None, None, 1.0, 1, 0, hold_us, 0.0, 1)      # one paced wave: GPU busy
+    t0 = time.perf_counter()
+    for _ in range(k):
+        one_step(False)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize(device)
+    ms = (t1 - t0) / k * 1e3
+    if ms * k * 1e3 > 0.9 * hold_us:
+        print(f"[host-check] enqueue took {ms * k:.1f} ms: a step waits for the GPU (host sync)", flush=True)
+    return ms
 
 
 def main(argv=None):

@@ -53,6 +53,12 @@ void dltb_transpose(const void* src, void* dst, int R, int C, hipStream_t st);
 void dltb_transpose_batched(const void* src, void* dst, int R, int C, int nb, long sbs, long dbs,
                             hipStream_t st);
 
+// comm_emu.hip: one emulated RCCL collective (DLTB_COMM=emulate:N) -- `channels` paced workgroups
+// that read `traffic` (`passes` times) and write dst[r * rep_stride + j] = scale * src[j]
+void dltb_comm_emu(const void* traffic, long traffic_bytes, int passes, void* dst, const void* src, long n,
+                   int elem, float scale, int replicas, long rep_stride, float alpha_us, float beta_us,
+                   int channels, hipStream_t st);
+
 // embedding.hip
 void dltb_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* x, int N, int T,
                     int d, uint32_t thr16, float scale, const int64_t* seed, int64_t site,

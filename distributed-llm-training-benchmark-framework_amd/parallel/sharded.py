@@ -172,10 +172,25 @@ class ShardedEngine(Engine):
         self._cache_wt = (self.world == 1 and self.accum > 1 and nparam < 2_000_000_000
                           and bool(cfg.extra.get("cache_weight_t", True)))
         if self.world > 1:
+            # modelled wire bytes one rank sends per micro-step (ring algorithms), per group: its
+            # all-gathers (once per optimizer step when everything stays gathered; once per
+            # micro-step for SHARD_GRAD_OP and the FSDP root group, which stays gathered from its
+            # forward through its backward; else forward + backward re-gather) and one reduce-scatter;
+            # the persistent (replicated) parameters: a reduce-scatter per micro-step and an
+            # all-gather per optimizer step
             e = self.shard_buf.element_size()
-            gathers = 1 if (self.keep_all or not cfg.reshard_after_forward) else 2
             frac = (self.world - 1) / self.world
-            self.comm_bytes_per_step = int(total_sharded * e * frac * (gathers + 1))
+            per = 0.0
+            for g in groups:
+                if self.keep_all:
+                    ng = 1.0 / self.accum
+                elif not cfg.reshard_after_forward or g.root:
+                    ng = 1.0
+                else:
+                    ng = 2.0
+                per += frac * g.total * e * (ng + 1.0)
+            per += frac * p_total * e * (1.0 + 1.0 / self.accum)
+            self.comm_bytes_per_step = int(per)
 
     def _slot_key(self, unit, i):
         """(buffer, element offset) of gradient slot ``i`` of ``unit`` at world size 1."""

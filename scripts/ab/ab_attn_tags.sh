@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Interleaved scripts/bench_attn.py A/B of attention builds (csrc/build.py --tag T): base vs each tag,
-# plus the attention GPU tests on the first tag.   scripts/ab_attn_tags.sh ROUNDS TAG [TAG...]
+# plus the attention GPU tests on the first tag.   scripts/ab/ab_attn_tags.sh ROUNDS TAG [TAG...]
 set -e
 mkdir -p gpurun_out
 R=$1; shift

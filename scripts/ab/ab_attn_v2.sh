@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # A/B of attention-kernel variants built by csrc/build.py --tag: numerics tests on the first
 # variant, then interleaved scripts/bench_attn.py runs and bench.py runs (DLTB_EXT_PATH selects).
-#   scripts/ab_attn_v2.sh TAG [TAG...]
+#   scripts/ab/ab_attn_v2.sh TAG [TAG...]
 set -e
 mkdir -p gpurun_out
 TAGS=("$@")

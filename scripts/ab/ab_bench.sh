@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
 # A/B a list of bench.py variants in one GPU session (one JSON line each, appended to $OUT).
-#   ./scripts/ab_bench.sh OUT.jsonl "ENV=1 --flag" "--other-flag" ...
+#   ./scripts/ab/ab_bench.sh OUT.jsonl "ENV=1 --flag" "--other-flag" ...
 # Each variant runs as its own process under a time limit; the script stops at the first failure.
 set -uo pipefail
-ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
 OUT="$1"; shift
 mkdir -p "$(dirname "$OUT")"
 for v in "$@"; do

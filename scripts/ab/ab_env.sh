@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
 # Per-kernel + bench A/B of an environment switch: rocprofv3 kernel stats of a short bench with
 # VAR=A and VAR=B (kernels matching PATTERN), then ROUNDS interleaved bench.py runs of each.
-#   scripts/ab_env.sh VAR A B PATTERN ROUNDS [bench flags...]
+#   scripts/ab/ab_env.sh VAR A B PATTERN ROUNDS [bench flags...]
 set -euo pipefail
-ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
 VAR=$1; A=$2; B=$3; PAT=$4; ROUNDS=$5; shift 5
 cd /tmp && export TMPDIR=/tmp
 for v in "$A" "$B"; do

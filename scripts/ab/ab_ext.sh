@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
 # A/B of a kernel variant built with `python csrc/build.py --tag TAG [-D ...]` against the release
 # extension: alternating bench.py runs on one box (DLTB_EXT_PATH selects the variant).
-#   scripts/ab_ext.sh TAG [ROUNDS] [bench.py flags...]
+#   scripts/ab/ab_ext.sh TAG [ROUNDS] [bench.py flags...]
 set -euo pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 TAG=$1; ROUNDS=${2:-3}; shift 2 || shift $#
 SO=$(ls build/$TAG/_C*.so)
 mkdir -p gpurun_out

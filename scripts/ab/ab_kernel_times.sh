@@ -1,9 +1,9 @@
 #!/usr/bin/env bash
 # Per-kernel A/B of an extension variant (build/TAG) vs the release build: rocprofv3 kernel stats of
 # the same short bench, one run each, and the lines of the kernels matching PATTERN.
-#   scripts/ab_kernel_times.sh TAG PATTERN [bench flags...]
+#   scripts/ab/ab_kernel_times.sh TAG PATTERN [bench flags...]
 set -euo pipefail
-ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+ROOT="$(cd "$(dirname "$0")/../.." && pwd)"
 TAG=$1; PAT=$2; shift 2
 SO=$(ls "$ROOT"/build/$TAG/_C*.so)
 cd /tmp && export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # A/B of functional.wgrad_operands (transposed K-contiguous operand for large weight gradients) on
 # the Mistral-7B-shape ZeRO-3 bench: "off" patches the gain model to zero in-process.
 set -euo pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 ARGS="--tier M7B --seq-len 4096 --strategy zero3 --steps 8 --warmup 4"
 for r in 1 2; do
   for mode in off on; do

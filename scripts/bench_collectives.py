@@ -69,7 +69,7 @@ def main():
         nbytes = int(size * (1 << 20))
         n = max(world, nbytes // esz // world * world)
         buf = torch.ones(n, dtype=dt, device=dev)
-        out = torch.empty(n // world if True else n, dtype=dt, device=dev)
+        out = torch.empty(n // world, dtype=dt, device=dev)
         for op in a.ops.split(","):
             o = out if op != "all_to_all" else torch.empty_like(buf)
             for _ in range(a.warmup):

@@ -1,0 +1,104 @@
+"""Emulated-fabric comm mode on the MI355X (DLTB_COMM=emulate:N, csrc/comm_emu.hip).
+
+* The paced collective kernel lasts its modelled duration (alpha + beta) within a few percent,
+  while its numerics stand-in matches the fp32 torch oracle for bf16 and fp32 buffers.
+* It runs on a separate stream: a compute kernel queued beside it overlaps it.
+* Every engine at emulate:4 on the GPU issues exactly its modelled wire bytes (the fp32-comm DDP
+  case only exists with 16-bit compute, so only here), trains with finite loss, and its
+  ``comm_wait`` / peak-HBM figures come out of bench.py.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import dltb  # noqa: F401
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _ext():
+    from dltb.ops._ext import ext
+    return ext()
+
+
+def _time_ms(fn, dev):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    fn()
+    e.record()
+    torch.cuda.synchronize(dev)
+    return s.elapsed_time(e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_paced_kernel_duration_and_numerics(dt):
+    dev = torch.device("cuda", 0)
+    C = _ext()
+    src = (torch.randn(1 << 20, device=dev)).to(dt)
+    dst = torch.empty(4 << 20, device=dev, dtype=dt)
+    C.comm_emu(src, 1, dst, src, 1.0, 1, 0, 5.0, 5.0, 32)           # warm-up
+    ms = _time_ms(lambda: C.comm_emu(src, 1, dst, src, 4.0, 4, 1 << 20, 200.0, 800.0, 32), dev)
+    assert 0.97 <= ms <= 1.15, ms                                     # 1000 us modelled
+    ref = (src.float() * 4.0).to(dt)
+    for r in range(4):
+        assert torch.equal(dst[r << 20:(r + 1) << 20], ref), r
+    # the one-float grad-norm all-reduce (scalar path), in place
+    t = torch.tensor([2.5], device=dev)
+    ms = _time_ms(lambda: C.comm_emu(t, 1, t, t, 8.0, 1, 0, 30.0, 0.0, 32), dev)
+    assert float(t.item()) == 20.0 and 0.025 <= ms <= 0.08, ms
+
+
+@pytest.mark.gpu
+def test_emulated_collective_overlaps_compute(monkeypatch):
+    monkeypatch.setenv("DLTB_COMM", "emulate:8")
+    monkeypatch.setenv("DLTB_EMU_ALPHA_US", "1000")                  # a 1 ms collective
+    from dltb.comm import Comm
+    dev = torch.device("cuda", 0)
+    c = Comm()
+    a = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    buf = torch.ones(1 << 16, device=dev, dtype=torch.bfloat16)
+    for _ in range(3):
+        a @ a
+    torch.cuda.synchronize(dev)
+    t_mm = _time_ms(lambda: [a @ a for _ in range(3)], dev)
+    t_cc = _time_ms(lambda: c.all_reduce(buf).wait(), dev)
+
+    def both():
+        w = c.all_reduce(buf)
+        for _ in range(3):
+            a @ a
+        w.wait()
+
+    buf.fill_(1.0)
+    t_both = _time_ms(both, dev)
+    assert t_cc >= 0.95
+    assert t_both < 0.9 * (t_mm + t_cc), (t_mm, t_cc, t_both)
+    assert torch.equal(buf, torch.full_like(buf, 8.0))
+
+
+def _bench(args, env_extra=None):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DLTB_COMM"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    return [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")][0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [["--strategy", "zero2"], ["--strategy", "ddp", "--dtype", "bf16", "--grad-comm-dtype", "fp32"],
+                                   ["--strategy", "zero3"], ["--strategy", "fsdp"]],
+                         ids=["zero2", "ddp-fp32comm", "zero3", "fsdp"])
+def test_bench_emulate4_wire_bytes(extra):
+    rec = _bench(["--emulate", "4", "--steps", "8", "--warmup", "4", "--seq-len", "512", *extra])
+    assert rec["prediction"] and rec["emulated_world"] == 4
+    assert abs(rec["wire_bytes_per_step"] - rec["wire_bytes_per_step_model"]) <= 16, rec
+    assert rec["mean_loss"] == rec["mean_loss"] and 0 < rec["mean_loss"] < 20
+    assert rec["comm_wait_ms"] is not None and rec["peak_hbm_gb_per_rank"] > 0
