@@ -11,7 +11,12 @@ ZeRO-3 with release + re-gather, FSDP per-block and the reference's root FlatPar
 Mistral-shape GQA model under ZeRO-3) the same model (same init) trains ``windows`` accumulation
 windows of ``accum`` micro-steps.  Rank r of N reads row r of each micro-step's [N_ref, T] token
 table; the world-1 run reads all rows as one batch, so the averaged gradients are mathematically
-identical.  Dropout is off (dropout masks are per-rank streams).  AdamW runs with eps = 1 and
+identical.  Dropout is off in the equivalence cases (dropout masks are per-rank streams, so a
+world-1 run cannot draw the same masks); the ``dropout`` case turns it on with every rank reading
+the SAME rows, which pins that ranks draw distinct masks (their losses differ), that a fixed seed
+is deterministic (tests/ re-run it) and that the loss stays within dropout noise of world 1.
+``zero3_m7b`` is the Mistral-7B layer at full width (d4096, GQA 32/8, SwiGLU 14336; 2 layers,
+vocab 8192) under ZeRO-3 -- BASELINE config #5's shapes through every sharded code path.  AdamW runs with eps = 1 and
 no weight decay, which makes an update ~ lr * gradient (not the sign of it), so comparing the
 parameter *updates* of two runs compares their reduced gradients.  Rank 0 writes
 {case: {"init", "final", "losses"}} (fp32, CPU) to ``--out``; tests/test_multirank_gpu.py compares
@@ -39,13 +44,21 @@ CASES = {
     "fsdp_root": dict(strategy="fsdp", wrap="root"),
     "zero3_mistral": dict(strategy="zero3", tier="mtiny", persist=1024),
 }
+EXTRA_CASES = {
+    "zero3_m7b": dict(strategy="zero3", tier="m7b_2l", persist=100_000),
+    "dropout": dict(strategy="zero2", dropout=0.1, same_rows=True),
+}
 
 
-def model_config(tier, seq_len):
+def model_config(tier, seq_len, dropout=0.0):
     from dltb.models import get_model_config
     if tier == "mtiny":
         return get_model_config("mtiny", seq_len)
-    c = get_model_config("A", seq_len, dropout=0.0)      # TinyGPT, narrowed: d256 / 4 heads of 64
+    if tier == "m7b_2l":                                 # Mistral-7B width, 2 layers, small vocab
+        c = get_model_config("M7B", seq_len)
+        c.n_layer, c.vocab_size = 2, 8192
+        return c
+    c = get_model_config("A", seq_len, dropout=dropout)  # TinyGPT, narrowed: d256 / 4 heads of 64
     c.n_embd, c.n_head, c.n_layer, c.vocab_size = 256, 4, 2, 4096
     return c
 
@@ -54,7 +67,7 @@ def run_case(name, spec, world, rank, device, a):
     from dltb.models import build_model
     from dltb.parallel import engine_config, make_engine
     torch.manual_seed(0)
-    mcfg = model_config(spec.get("tier", "A"), a.seq_len)
+    mcfg = model_config(spec.get("tier", "A"), a.seq_len, spec.get("dropout", 0.0))
     with torch.device(device):
         model = build_model(mcfg)
     init = {n: p.detach().float().cpu().clone() for n, p in model.named_parameters()}
@@ -75,22 +88,26 @@ def run_case(name, spec, world, rank, device, a):
     steps = a.windows * a.accum
     table = torch.randint(0, mcfg.vocab_size, (steps, a.ref_batch, a.seq_len), generator=g)
     per = a.ref_batch // world
-    losses = []
+    same = spec.get("same_rows", False)
+    losses, rank_losses = [], []
     for k in range(steps):
-        b = table[k, rank * per:(rank + 1) * per].to(device)
+        # same_rows: every rank (and every row of the world-1 batch) reads row 0 of the micro-step
+        b = (table[k, :1].expand(per, -1).contiguous() if same else table[k, rank * per:(rank + 1) * per]).to(device)
         loss = eng(b, b)[1]
         eng.backward(loss)
         eng.step()
-        lv = torch.tensor([float(loss.item())], dtype=torch.float64)
+        lv = torch.zeros(world, dtype=torch.float64)
+        lv[rank] = float(loss.item())
         if world > 1:
             dist.all_reduce(lv)
-        losses.append(float(lv.item()) / world)
+        rank_losses.append(lv.tolist())
+        losses.append(float(lv.sum()) / world)
     eng.finalize()
     sd = eng.full_state_dict()
     final = {n: t.detach().float().cpu() for n, t in sd.items()}
     del eng, model
     torch.cuda.empty_cache() if device.type == "cuda" else None
-    return {"init": init, "final": final, "losses": losses}
+    return {"init": init, "final": final, "losses": losses, "rank_losses": rank_losses}
 
 
 def main():
@@ -114,7 +131,7 @@ def main():
     out = {}
     try:
         for name in a.cases.split(","):
-            out[name] = run_case(name, CASES[name], world, rank, device, a)
+            out[name] = run_case(name, {**CASES, **EXTRA_CASES}[name], world, rank, device, a)
             if rank == 0:
                 print(f"[multirank_check] ws={world} {name}: losses {['%.4f' % v for v in out[name]['losses']]}",
                       flush=True)

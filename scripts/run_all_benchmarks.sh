@@ -16,18 +16,24 @@
 #                                 (configs/fsdp/fsdp_reference_root.yaml)
 #       ddp_uniform fsdp_uniform  DDP / FSDP with ZeRO semantics (grad-accum 4, clip 1.0, WarmupLR)
 #       zero1                     ZeRO-2 engine with one reduce-scatter per window (opt-in row)
+#  2b. BASELINE config #5: Mistral-7B-shape ZeRO-3 (tier M7B, seq 4096) with the reference's
+#      zero3.json and with configs/deepspeed/zero3_mi355x_288gb.json (gathered parameters stay
+#      resident in 288 GB), rows zero3_m7b / zero3_m7b_288gb at M7B_WS (default "1 8");
+#      trainable_params and per-rank peak HBM land in each row's .extended.json sidecar.
+#      M7B=0 skips it; M7B_TIER / M7B_SEQ / M7B_STEPS override (the CPU rehearsal uses mtiny).
 #  3. parse -> plot -> report.
 # Like the reference it always exits 0; failed configs are listed in results/summary/failures.json.
 #
 #   ./scripts/run_all_benchmarks.sh [results-dir]
 #   env: STEPS, SEQ, TIER, WS_LIST, STRATS, TIMEOUT, HARNESS_EXTRA (extra harness flags),
+#        M7B, M7B_WS, M7B_TIER, M7B_SEQ, M7B_STEPS (step 2b),
 #        FORCE_NPROC (process slots when no GPU is visible, e.g. the gloo/CPU rehearsal),
 #        COLLECTIVES=0 (skip step 1), COLL_MAX_MB (largest swept message, default 512)
 set -uo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 RESULTS="${1:-$ROOT/results}"
 STEPS="${STEPS:-100}"; SEQ="${SEQ:-2048}"; TIER="${TIER:-A}"; TIMEOUT="${TIMEOUT:-900}"
-STRATS="${STRATS:-ddp fsdp zero2 zero3 fsdp_root ddp_bf16 fsdp_bf16 ddp_uniform fsdp_uniform}"
+STRATS="${STRATS-ddp fsdp zero2 zero3 fsdp_root ddp_bf16 fsdp_bf16 ddp_uniform fsdp_uniform}"
 NGPU="${FORCE_NPROC:-$(python3 -c "import torch; print(torch.cuda.device_count())" 2>/dev/null || echo 0)}"
 read -r -a HX <<< "${HARNESS_EXTRA:-}"
 WS_LIST="${WS_LIST:-1 2 4 8}"
@@ -107,6 +113,28 @@ for s in $STRATS; do
     fi
   done
 done
+# ---- 2b. BASELINE config #5: Mistral-7B-shape ZeRO-3 at 1 and 8 GPUs
+if [[ "${M7B:-1}" != "0" ]]; then
+  M7B_TIER="${M7B_TIER:-M7B}"; M7B_SEQ="${M7B_SEQ:-4096}"; M7B_STEPS="${M7B_STEPS:-20}"
+  for row in zero3_m7b zero3_m7b_288gb; do
+    cfg="$ROOT/configs/deepspeed/zero3.json"
+    [[ "$row" == zero3_m7b_288gb ]] && cfg="$ROOT/configs/deepspeed/zero3_mi355x_288gb.json"
+    for ws in ${M7B_WS:-1 8}; do
+      if [[ "$ws" -gt "$NGPU" ]]; then echo "skip $row ws=$ws (only $NGPU GPUs)"; continue; fi
+      job="bench-master-${row}-ws${ws}-seq${M7B_SEQ}"
+      echo "---- $job"
+      if timeout -k 30 "$((2 * TIMEOUT))" "$ROOT/scripts/launch_local.sh" --strategy zero3 --world-size "$ws" \
+           --seq-len "$M7B_SEQ" --tier "$M7B_TIER" --steps "$M7B_STEPS" --per-device-batch 1 --grad-accum 4 \
+           --results-dir "$RESULTS/raw" -- --deepspeed-config "$cfg" --strategy-label "$row" "${HX[@]}" \
+           > "$RESULTS/$job.log" 2>&1 \
+         && "$ROOT/scripts/collect_results.sh" "$RESULTS/$job.log" "$RESULTS" "$job" "$RESULTS/raw"; then
+        DONE=$((DONE + 1)); echo "     ok"
+      else
+        FAILED+=("$job"); echo "     FAILED (see $RESULTS/$job.log)"; tail -20 "$RESULTS/$job.log" || true
+      fi
+    done
+  done
+fi
 python3 - "$RESULTS/summary/failures.json" "${FAILED[@]}" <<'PY'
 import json, sys
 json.dump({"failed": sys.argv[2:]}, open(sys.argv[1], "w"), indent=2)

@@ -61,3 +61,22 @@ def compare(ref, got, loss_tol, upd_tol, cos_min, param_tol):
                 if pr > param_tol:
                     bad.append((case, n, pr))
     return bad
+
+
+def report(ref, got):
+    """Per case: max relative loss gap, update rel-L2 / cosine and the largest per-parameter update
+    gap (the quantities ``compare`` bounds), for recording how tight a run actually is."""
+    out = {}
+    for case, r in ref.items():
+        g = got[case]
+        ur = {n: r["final"][n] - r["init"][n] for n in r["init"]}
+        ug = {n: g["final"][n] - g["init"][n] for n in r["init"]}
+        vr = torch.cat([ur[n].reshape(-1) for n in ur]).double()
+        vg = torch.cat([ug[n].reshape(-1) for n in ur]).double()
+        top = max(ur[n].norm().item() for n in ur)
+        prel = max(((ug[n] - ur[n]).norm() / ur[n].norm()).item() for n in ur if ur[n].norm().item() >= 0.05 * top)
+        out[case] = {"loss_rel": max(abs(a - b) / abs(a) for a, b in zip(r["losses"], g["losses"])),
+                     "upd_rel": ((vg - vr).norm() / vr.norm()).item(),
+                     "upd_cos": (torch.dot(vg, vr) / (vg.norm() * vr.norm())).item(),
+                     "param_rel_max": prel}
+    return out

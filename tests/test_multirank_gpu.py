@@ -5,9 +5,12 @@ persistent small params), FSDP per-block and root, Mistral-shape GQA under ZeRO-
 HIP kernels, batched weight gradients per bucket, deferred all-gathers and fp32 accumulation of
 reduce-scattered chunks.  After 3 windows the parameter updates must match the world-1 GPU run on
 the concatenated batch within bf16 tolerance (reference: train_harness.py:210-271)."""
-import pytest
+import json
 
-from multirank_util import compare, run
+import pytest
+import torch
+
+from multirank_util import compare, report, run
 
 pytestmark = pytest.mark.gpu
 
@@ -16,6 +19,7 @@ def test_world2_host_staged_equals_world1_gpu(tmp_path):
     ws1 = run(tmp_path / "ws1.pt", 1, "cuda", timeout=600)
     ws2 = run(tmp_path / "ws2.pt", 2, "cuda", env_extra={"DLTB_COMM": "host"}, timeout=600)
     assert set(ws1) == set(ws2)
+    print("[multirank] host-staged ws2 vs ws1:", json.dumps(report(ws1, ws2)))
     bad = compare(ws1, ws2, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
     assert not bad, bad
     # DLTB_DEFER_OPT=0: the ZeRO-1/2 update + all-gather at the boundary instead of deferred into
@@ -31,3 +35,26 @@ def test_world2_host_staged_equals_world1_gpu(tmp_path):
     ws2l = run(tmp_path / "ws2l.pt", 2, "cuda", env_extra={"DLTB_COMM": "host", "DLTB_COMM_LAZY": "1"}, timeout=600)
     bad = compare({k: ws1[k] for k in ws2l}, ws2l, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
     assert not bad, bad
+
+
+def test_world2_m7b_width_and_dropout(tmp_path):
+    """BASELINE config #5's layer shapes at full width (d4096, GQA 32/8, SwiGLU 14336; 2 layers)
+    under ZeRO-3 at world 2 == world 1; and dropout streams: distinct per rank, deterministic,
+    loss within dropout noise of world 1 (scripts/multirank_check.py EXTRA_CASES)."""
+    ex = ("--cases", "zero3_m7b")
+    ws1 = run(tmp_path / "m1.pt", 1, "cuda", extra=ex, timeout=600)
+    ws2 = run(tmp_path / "m2.pt", 2, "cuda", extra=ex, env_extra={"DLTB_COMM": "host"}, timeout=600)
+    print("[multirank] zero3_m7b ws2 vs ws1:", json.dumps(report(ws1, ws2)))
+    bad = compare(ws1, ws2, loss_tol=1e-2, upd_tol=0.08, cos_min=0.995, param_tol=0.2)
+    assert not bad, bad
+    ex = ("--cases", "dropout")
+    d1 = run(tmp_path / "d1.pt", 1, "cuda", extra=ex, timeout=600)["dropout"]
+    da = run(tmp_path / "da.pt", 2, "cuda", extra=ex, env_extra={"DLTB_COMM": "host"}, timeout=600)["dropout"]
+    db = run(tmp_path / "db.pt", 2, "cuda", extra=ex, env_extra={"DLTB_COMM": "host"}, timeout=600)["dropout"]
+    for r0, r1 in da["rank_losses"]:
+        assert r0 != r1, "ranks drew the same dropout masks"
+    assert da["rank_losses"] == db["rank_losses"]
+    for n in da["final"]:
+        assert torch.equal(da["final"][n], db["final"][n]), n
+    for l1, l2 in zip(d1["losses"], da["losses"]):
+        assert abs(l1 - l2) < 0.02 * abs(l1), (l1, l2)

@@ -9,10 +9,10 @@ import pandas as pd
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _suite(tmp_path, extra, strats="ddp zero2"):
+def _suite(tmp_path, extra, strats="ddp zero2", m7b="0"):
     env = dict(os.environ, STEPS="6", SEQ="64", TIER="tiny", WS_LIST="1 2", STRATS=strats, FORCE_NPROC="2",
                HARNESS_EXTRA=f"--device cpu --warmup-steps 2 --log-every 0 {extra}", TIMEOUT="300",
-               OMP_NUM_THREADS="1")
+               OMP_NUM_THREADS="1", M7B=m7b, M7B_TIER="mtiny", M7B_SEQ="64", M7B_STEPS="6", M7B_WS="1 2")
     r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "run_all_benchmarks.sh"), str(tmp_path)],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -57,3 +57,16 @@ def test_suite_variant_rows_and_measured_bucket_profile(tmp_path, monkeypatch):
     assert ext["engine_config"]["wrap"] == "root" and ext["strategy_engine"] == "fsdp"
     ext = json.load(open(tmp_path / "bench-master-ddp_uniform-ws2-seq64_results" / "result.extended.json"))
     assert ext["engine_config"]["grad_accum"] == 4 and ext["accum_semantics"] == "uniform"
+
+
+def test_suite_m7b_rows(tmp_path):
+    """Step 2b (BASELINE config #5): the Mistral-shape ZeRO-3 rows with the reference's zero3.json
+    and the 288 GB config, rehearsed at the mtiny shape; trainable params + per-rank peak in the
+    sidecar."""
+    _suite(tmp_path, "", strats="", m7b="1")
+    df = pd.read_csv(tmp_path / "summary" / "metrics.csv")
+    assert sorted(zip(df.strategy, df.world_size)) == [("zero3_m7b", 1), ("zero3_m7b", 2),
+                                                       ("zero3_m7b_288gb", 1), ("zero3_m7b_288gb", 2)]
+    assert json.load(open(tmp_path / "summary" / "failures.json")) == {"failed": []}
+    ext = json.load(open(tmp_path / "bench-master-zero3_m7b_288gb-ws2-seq64_results" / "result.extended.json"))
+    assert ext["trainable_params"] > 0 and ext["peak_vram_reserved_gb"] is not None
