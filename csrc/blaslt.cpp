@@ -36,13 +36,24 @@ hipblasLtHandle_t handle() {
 }
 
 // One split-K workspace per stream: two tuned split-K GEMMs running concurrently on different
-// streams must not share their partials buffer.
+// streams must not share their partials buffer.  A stream first seen while it is being captured
+// into a HIP graph (torch captures on a side stream of its own, and nothing may be allocated
+// during a capture) gets the first stream's workspace: a graph replays on the stream that enqueues
+// it, in order with that stream's eager work.
 void* workspace(hipStream_t st) {
   static std::map<hipStream_t, void*> ws;
+  static void* first = nullptr;
   auto it = ws.find(st);
   if (it != ws.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    if (!first) throw std::runtime_error("blaslt: first GEMM inside a graph capture (run one eagerly first)");
+    ws.emplace(st, first);
+    return first;
+  }
   void* p = nullptr;
   if (hipMalloc(&p, kWorkspace) != hipSuccess) throw std::runtime_error("blaslt workspace alloc failed");
+  if (!first) first = p;
   ws.emplace(st, p);
   return p;
 }
