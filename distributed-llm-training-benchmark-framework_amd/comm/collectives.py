@@ -250,6 +250,15 @@ class Comm:
         off = out.data_ptr() + self.rank * n * out.element_size()
         if inp.data_ptr() == off and inp.dtype == out.dtype:     # in place: the own chunk is already there
             return self._emu("all_gather", out, async_op=async_op, track=track)
+        if out.is_cuda and out.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            # integer payloads (the embedding's token ids): replicate with a torch copy on the
+            # emulation stream, the paced kernel models the transfer
+            if self._emu_stream is None:
+                self._emu_stream = torch.cuda.Stream(device=out.device, priority=-1)
+            self._emu_stream.wait_stream(torch.cuda.current_stream(out.device))
+            with torch.cuda.stream(self._emu_stream):
+                out.view(self.world, n).copy_(inp.reshape(1, n).expand(self.world, n))
+            return self._emu("all_gather", out, async_op=async_op, track=track)
         return self._emu("all_gather", out, out.view(-1), inp.reshape(-1), 1.0, self.world, n,
                          async_op=async_op, track=track)
 

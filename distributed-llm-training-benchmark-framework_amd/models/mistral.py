@@ -81,10 +81,7 @@ class _EmbedFn(torch.autograd.Function):
         model = ctx.model
         rt, unit = model.rt, model.unit_embed
         rt.acquire_backward(unit)
-        dwte, acc = rt.grad_slot(unit, 0)
-        if not acc:
-            dwte.zero_()
-        F_.embed_bwd(dx.contiguous(), ctx.idx, dwte, None, False, 0.0, rt.seed, 0)
+        rt.embedding_backward((unit, 0), None, dx.contiguous(), ctx.idx, 0.0, rt.seed, 0)
         rt.grads_ready(unit)
         rt.release_backward(unit)
         return None, None, None

@@ -71,10 +71,18 @@ class TinyGPTBlock(nn.Module):
 
 
 class _EmbedFn(torch.autograd.Function):
+    """Token + position embedding.  The tied token table is a parameter of the HEAD unit (whose
+    backward runs first and writes its dense gradient), so engines reduce it right after the
+    head, under all block backwards; this unit owns only the position table.  The token rows of
+    this backward are handed to ``rt.embedding_backward``: added to the head's dense part in place,
+    or -- where the table's collective already ran -- exchanged sparsely (parallel/replicated.py,
+    parallel/sharded.py)."""
+
     @staticmethod
     def forward(ctx, anchor, idx, model):
         rt, unit = model.rt, model.unit_embed
-        wte, wpe = rt.acquire(unit)
+        wte = rt.acquire_tied(model.unit_head)[2]
+        (wpe,) = rt.acquire(unit)
         p = model.drop_p
         x = F_.embed_fwd(idx, wte, wpe, p, rt.seed, model.site_embed)
         rt.release_forward(unit)
@@ -86,11 +94,8 @@ class _EmbedFn(torch.autograd.Function):
         model = ctx.model
         rt, unit = model.rt, model.unit_embed
         rt.acquire_backward(unit)
-        dwte, acc_wte = rt.grad_slot(unit, 0)
-        dwpe, acc_wpe = rt.grad_slot(unit, 1)
-        if not acc_wte:
-            dwte.zero_()
-        F_.embed_bwd(dx.contiguous(), ctx.idx, dwte, dwpe, acc_wpe, model.drop_p, rt.seed, model.site_embed)
+        rt.embedding_backward((model.unit_head, 2), (unit, 0), dx.contiguous(), ctx.idx, model.drop_p, rt.seed,
+                              model.site_embed)
         rt.grads_ready(unit)
         rt.release_backward(unit)
         return None, None, None
@@ -205,8 +210,7 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_in, m_in, model, targets, return_logits):
         rt = model.rt
-        lnw, lnb = rt.acquire(model.unit_head)
-        wte = rt.acquire_tied(model.unit_embed)[0]
+        lnw, lnb, wte = rt.acquire(model.unit_head)
         if m_in is None:
             x = x_in
             _, h, mean, rstd = F_.norm_fwd(x, None, lnw, lnb, LN_EPS, False)
@@ -239,12 +243,11 @@ class _HeadFn(torch.autograd.Function):
         rt = model.rt
         (x, h, mean, rstd, dl, count) = ctx.saved
         ctx.saved = None
-        lnw, lnb = rt.acquire_backward(model.unit_head)
-        wte = rt.acquire_tied(model.unit_embed)[0]
-        dw, acc_w = rt.grad_slot(model.unit_embed, 0)            # tied lm_head / wte
+        lnw, lnb, wte = rt.acquire_backward(model.unit_head)
+        dw, acc_w = rt.grad_slot(model.unit_head, 2)             # tied lm_head / wte (dense part)
         hs, g = F_.scale_by(h, dloss, count)                      # g = dloss / count (device)
         F_.linear_wgrad(dl, hs, dw, None, acc_w)
-        dh = F_.head_dgrad(dl, wte, rt.weight_t(model.unit_embed, 0, wte), g)
+        dh = F_.head_dgrad(dl, wte, rt.weight_t(model.unit_head, 2, wte), g)
         gw, acc = rt.grad_slot(model.unit_head, 0)
         gb, _ = rt.grad_slot(model.unit_head, 1)
         dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False)
@@ -295,12 +298,14 @@ class TinyGPT(nn.Module):
 
     def _build_units(self):
         t = self.transformer
-        self.unit_embed = Unit("embed", [("transformer.wte.weight", t["wte"].weight),
-                                         ("transformer.wpe.weight", t["wpe"].weight)], 0)
+        # the tied token table (wte = lm_head.weight) is the head unit's third parameter: the head's
+        # backward, the first of the step, completes its dense gradient (see _EmbedFn)
+        self.unit_embed = Unit("embed", [("transformer.wpe.weight", t["wpe"].weight)], 0)
         self.unit_blocks = [Unit(f"h.{i}", [(f"transformer.h.{i}.{n}", p) for n, p in blk.param_list()], i + 1)
                             for i, blk in enumerate(t["h"])]
         self.unit_head = Unit("head", [("transformer.ln_f.weight", t["ln_f"].weight),
-                                       ("transformer.ln_f.bias", t["ln_f"].bias)], len(self.unit_blocks) + 1)
+                                       ("transformer.ln_f.bias", t["ln_f"].bias),
+                                       ("transformer.wte.weight", t["wte"].weight)], len(self.unit_blocks) + 1)
 
     def units(self):
         """Units in forward order (the engines reverse it for backward-ordered buckets)."""

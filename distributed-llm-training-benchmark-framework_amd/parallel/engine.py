@@ -79,7 +79,8 @@ class Engine(ParamRuntime):
         self.grad_norm = None
         self._norm_sq = torch.zeros(1, device=self.device, dtype=torch.float32)
         self._gscale = torch.ones(1, device=self.device, dtype=torch.float32)
-        self.comm_bytes_per_step = 0
+        self._comm_static = 0            # modelled wire bytes per micro-step (set by the engines)
+        self._sparse_model = 0.0         # + the token-row exchange (parallel/replicated.py), per micro-step
         self.timers = None               # utils.timers.PhaseTimers while the harness times phases
         self._reported = set()   # id(unit) of the units whose backward reported this micro-step
         self._cache_wt = False   # subclasses: True where parameters stay resident between steps
@@ -88,6 +89,22 @@ class Engine(ParamRuntime):
         self._wt_epoch = -1      # optimizer step the cached transposes belong to
         model.rt = self
         self._setup()
+
+    @property
+    def comm_bytes_per_step(self) -> int:
+        """Modelled wire bytes one rank sends per micro-step (ring algorithms): the engine's static
+        collectives plus, once the batch shape is known, the sparse token-row exchange."""
+        return int(self._comm_static + self._sparse_model)
+
+    @comm_bytes_per_step.setter
+    def comm_bytes_per_step(self, v):
+        self._comm_static = v
+
+    def _model_sparse(self, rows: int, d: int, elem: int, idx_elem: int, every: float):
+        """Model of the token-row exchange: two all-gathers (rows x d, rows ids) per exchange,
+        ``every`` exchanges per micro-step."""
+        frac = (self.world - 1) / self.world
+        self._sparse_model = frac * self.world * rows * (d * elem + idx_elem) * every
 
     def _phase(self, name: str):
         if self.timers is not None:

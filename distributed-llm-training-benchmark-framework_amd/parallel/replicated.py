@@ -64,7 +64,7 @@ class ReplicatedEngine(Engine):
         # rounded up to a multiple of 4 of the model's repeated unit (64 MiB -> 4 blocks, 101 MB).
         # Only the embedding (the unit that finishes last) then keeps a bucket of its own: a solo block 0
         # would be a 1-block batch (110 us) and leave 3 blocks for the group before it.
-        mult = int(cfg.extra.get("bucket_unit_multiple", 4))
+        mult = int(cfg.extra.get("bucket_unit_multiple", os.environ.get("DLTB_BUCKET_UNIT_MULTIPLE", 4)))
         solo_tail = 2
         if self.world > 1 and self.defer_wgrad and bucket_elems > 0 and mult > 1:
             sizes = sorted(u.numel for u in units)
@@ -75,7 +75,8 @@ class ReplicatedEngine(Engine):
             solo_tail = 1
         shard = self.stage >= 1
         self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
-                                      solo_tail=int(cfg.extra.get("solo_tail_units", solo_tail)))
+                                      solo_tail=int(cfg.extra.get("solo_tail_units",
+                                                                  os.environ.get("DLTB_SOLO_TAIL", solo_tail))))
         dev, dt = self.device, self.compute_dtype
         master_full = torch.zeros(L.total, dtype=torch.float32, device=dev)
         for s in L.slots.values():
@@ -145,6 +146,7 @@ class ReplicatedEngine(Engine):
         self._tail_defer = (self.stage == 2 and self.world > 1 and self.acc is not None and
                             bool(cfg.extra.get("defer_tail_reduce", True)))
         self._rs_inflight = {}   # bucket -> (work, first micro-step of its window)
+        self._sparse = None      # (token slot, gathered rows, gathered ids, works) of this backward
         nbytes = L.total * (4 if self.comm_f32 is not None else elem)
         if self.world > 1:
             # modelled wire bytes one rank sends per micro-step (ring algorithms): DDP one all-reduce
@@ -213,6 +215,73 @@ class ReplicatedEngine(Engine):
         # (micro-steps without a collective -- inside a ZeRO-1 / window-reduced accumulation
         # window -- leave every dW queued for the single batched flush at the end of the backward)
 
+    def embedding_backward(self, tok, pos, dx, idx, p, seed, site):
+        """The tied token table's bucket is reduced right after the head's backward (it sits in the
+        first bucket); when that collective already ran this micro-step, the embedding's token rows
+        are exchanged instead: this rank's rows after the dropout backward and its token ids are
+        all-gathered (world x 2048 x 1024 bf16 = 4 MB per rank at TinyGPT-A, instead of the 65.5 MB
+        dense table reduced after the last backward op) and every rank scatter-adds all of them
+        into the reduced gradient in ``_finish_backward`` (``_apply_sparse``)."""
+        b = self._bucket_of.get(id(tok[0]))
+        if self.world > 1 and b is not None and (pos is None or self._bucket_of.get(id(pos[0])) != b):
+            # structurally exchanged: every micro-step (ZeRO-2) or at each window boundary
+            self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(),
+                               1.0 if self.stage == 2 else 1.0 / self.accum)
+        if self.world == 1 or b is None or not (self._reduce_now() and b < self._next):
+            return super().embedding_backward(tok, pos, dx, idx, p, seed, site)
+        d = dx.shape[-1]
+        dx2 = dx.reshape(-1, d)
+        rows = F_.dropout(None, dx2, p, seed, site) if p > 0 else dx2.contiguous()
+        if pos is not None:
+            dwpe, acc_p = self.grad_slot(*pos)
+            F_.embed_bwd(dx, idx, None, dwpe, acc_p, p, seed, site)
+        rows_all = rows.new_empty((self.world * rows.shape[0], d))
+        idx_all = idx.new_empty((self.world * idx.shape[0], idx.shape[1]))
+        works = [self.comm.all_gather(rows_all, rows, track=False),
+                 self.comm.all_gather(idx_all.view(-1), idx.reshape(-1).contiguous(), track=False)]
+        self._sparse = (tok, rows_all, idx_all, works)
+
+    def _apply_sparse(self):
+        """Scatter-add the gathered token rows into the reduced token-table gradient: DDP into the
+        all-reduced buffer (bf16 in place, or through a bf16 scratch into the fp32 one), ZeRO-1/2
+        into this rank's owner chunk (the slot's range of the flat gradient is free again once its
+        reduce-scatter has read it, and serves as the scratch).  Every rank adds the same rows in
+        the same order: the result is identical on all ranks and deterministic."""
+        tok, rows_all, idx_all, works = self._sparse
+        self._sparse = None
+        for w in works:
+            w.wait()
+        s = self.layout.slot(*tok)
+        region = self.flat_grad[s.offset:s.offset + s.numel]
+        if self.stage == 0 and self.comm_f32 is None:
+            F_.embed_bwd(rows_all, idx_all, region.view(s.shape), None, False, 0.0, None, 0)
+            return
+        region.zero_()
+        F_.embed_bwd(rows_all, idx_all, region.view(s.shape), None, False, 0.0, None, 0)
+        if self.stage == 0:
+            dst = self.comm_f32[s.offset:s.offset + s.numel]
+            if dst.is_cuda:
+                ext().f32_from_bf16_(dst, region, True)
+            else:
+                dst += region.float()
+            return
+        b = self._bucket_of[id(tok[0])]
+        bk = self.layout.buckets[b]
+        c0 = bk.start + self.rank * bk.chunk
+        lo, hi = max(c0, s.offset), min(c0 + bk.chunk, s.offset + s.numel)
+        if hi <= lo:
+            return
+        src = self.flat_grad[lo:hi]
+        o = bk.owner_start + (lo - c0)
+        if self._tail_defer:                      # acc already holds this micro-step's chunk
+            dst = self.acc[o:o + hi - lo]
+            if dst.is_cuda:
+                ext().f32_from_bf16_(dst, src, True)
+            else:
+                dst += src.float()
+        else:                                     # rs_out, before it is folded into acc (if any)
+            self.rs_out[o:o + hi - lo] += src
+
     def _launch(self, b):
         if b in self._rs_inflight:
             self._drain_bucket(b)     # the previous micro-step's reduce-scatter of this bucket
@@ -267,6 +336,11 @@ class ReplicatedEngine(Engine):
                 self._launch(b)
         self._phase("comm_wait_begin")
         self._wait_works()
+        if self._sparse is not None:
+            b = self._bucket_of[id(self._sparse[0][0])]
+            if b in self._rs_inflight:
+                self._drain_bucket(b)          # the token table's chunk first, then its sparse rows
+            self._apply_sparse()
         if self._tail_defer and self._is_boundary:
             self._drain_all()                   # the optimizer reads the window's full sum next
         self._phase("comm_wait_end")

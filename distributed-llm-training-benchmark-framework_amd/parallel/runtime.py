@@ -111,6 +111,20 @@ class ParamRuntime:
         from ..ops import functional as F_
         F_.linear_wgrad(dy, x, dw, None, accumulate)
 
+    def embedding_backward(self, tok, pos, dx: torch.Tensor, idx: torch.Tensor, p: float, seed, site: int):
+        """The token-embedding backward: scatter-add the (dropout-backward'd) rows of ``dx`` into the
+        token table's gradient slot ``tok = (unit, i)`` by ``idx``, and their per-position sums
+        into the position table's slot ``pos`` (or None).  When the token table is tied to the
+        head, its slot already holds the head's dense gradient and the rows are added to it.
+        Engines whose collective for ``tok`` already ran this micro-step (the tied table is
+        reduced right after the head's backward) override this with a sparse exchange."""
+        from ..ops import functional as F_
+        dwte, acc = self.grad_slot(*tok)
+        if not acc:
+            dwte.zero_()
+        dwpe, acc_p = self.grad_slot(*pos) if pos is not None else (None, False)
+        F_.embed_bwd(dx, idx, dwte, dwpe, acc_p, p, seed, site)
+
     def grads_ready(self, unit: Unit):
         pass
 

@@ -153,6 +153,9 @@ class ShardedEngine(Engine):
                                if any(self._persistent(u, i) for i in range(len(u.params)))])
         self._p_left = self._p_pending
         self._held_grads = []
+        self._reduced = set()        # group ids reduce-scattered in this micro-step
+        self._p_reduced = False      # the persistent block reduce-scattered in this micro-step
+        self._sparse = None          # (token slot, persistent?, gathered rows, gathered ids, works)
         # single process: the dW products of all blocks run as strided-batched GEMMs at the end of
         # backward (parallel/wgrad.py); with shards, each group's gradient is reduce-scattered the
         # moment it is complete, so they are issued immediately
@@ -327,9 +330,57 @@ class ShardedEngine(Engine):
         if g.bwd_left == 0:
             self._reduce_group(g)
 
+    def embedding_backward(self, tok, pos, dx, idx, p, seed, site):
+        """As the replicated engines (parallel/replicated.py): when the token table's group (or the
+        persistent block, for a small table) was already reduce-scattered this micro-step -- ZeRO-3
+        reduces the head's group right after the head's backward -- the token rows and ids are
+        all-gathered and scatter-added into this rank's owner shard in ``_finish_backward``."""
+        unit, i = tok
+        persistent = (id(unit), i) in self.p_layout.slots
+        done = self._p_reduced if persistent else self._group_of[id(unit)].gid in self._reduced
+        if self.world > 1 and not persistent and (pos is None or self._group_of[id(pos[0])] is not self._group_of[id(unit)]):
+            self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(), 1.0)
+        if self.world == 1 or not done:
+            return super().embedding_backward(tok, pos, dx, idx, p, seed, site)
+        from ..ops import functional as F_
+        d = dx.shape[-1]
+        dx2 = dx.reshape(-1, d)
+        rows = F_.dropout(None, dx2, p, seed, site) if p > 0 else dx2.contiguous()
+        if pos is not None:
+            dwpe, acc_p = self.grad_slot(*pos)
+            F_.embed_bwd(dx, idx, None, dwpe, acc_p, p, seed, site)
+        rows_all = rows.new_empty((self.world * rows.shape[0], d))
+        idx_all = idx.new_empty((self.world * idx.shape[0], idx.shape[1]))
+        works = [self.comm.all_gather(rows_all, rows, track=False),
+                 self.comm.all_gather(idx_all.view(-1), idx.reshape(-1).contiguous(), track=False)]
+        self._sparse = (tok, persistent, rows_all, idx_all, works)
+
+    def _apply_sparse(self):
+        """Gathered token rows -> a transient dense table -> this rank's chunk of it added into
+        its owner gradient (rs_out, before it is folded into the fp32 accumulator)."""
+        from ..ops import functional as F_
+        (unit, i), persistent, rows_all, idx_all, works = self._sparse
+        self._sparse = None
+        for w in works:
+            w.wait()
+        if persistent:
+            sl, c0, chunk, base = self.p_layout.slot(unit, i), self.rank * self.p_layout.owner_numel, \
+                self.p_layout.owner_numel, 0
+        else:
+            g = self._group_of[id(unit)]
+            sl, c0, chunk, base = g.layout.slot(unit, i), self.rank * g.chunk, g.chunk, g.owner_start
+        lo, hi = max(c0, sl.offset), min(c0 + chunk, sl.offset + sl.numel)
+        if hi <= lo:
+            return
+        dense = torch.zeros(sl.shape, dtype=self.rs_out.dtype, device=self.rs_out.device)
+        F_.embed_bwd(rows_all, idx_all, dense, None, False, 0.0, None, 0)
+        o = base + (lo - c0)
+        self.rs_out[o:o + hi - lo] += dense.view(-1)[lo - sl.offset:hi - sl.offset]
+
     def _reduce_group(self, g):
         if g.grad is None:
             return
+        self._reduced.add(g.gid)
         if self.world > 1:
             out = self.rs_out[g.owner_start:g.owner_start + g.chunk]
             self.comm.reduce_scatter(out, g.grad)
@@ -340,6 +391,7 @@ class ShardedEngine(Engine):
         pc = self.p_layout.owner_numel
         if pc == 0:
             return
+        self._p_reduced = True
         if self.world > 1:
             self.comm.reduce_scatter(self.rs_out[:pc], self.p_grad)
         else:
@@ -354,6 +406,8 @@ class ShardedEngine(Engine):
 
     # ------------------------------------------------------------------ step lifecycle
     def _on_begin_micro(self):
+        self._reduced.clear()
+        self._p_reduced = False
         if self.world > 1:
             self._written.clear()    # full gradient buffers are reduced every micro-step
         # ws == 1: the group gradient buffers ARE the owner gradients; accumulate in place
@@ -371,6 +425,8 @@ class ShardedEngine(Engine):
             g.bwd_left = len(g.units)
         self._phase("comm_wait_begin")
         self._wait_works()
+        if self._sparse is not None:
+            self._apply_sparse()
         self._phase("comm_wait_end")
         self._held_grads.clear()
         if self.acc is not None:

@@ -102,3 +102,19 @@ def test_bench_emulate4_wire_bytes(extra):
     assert abs(rec["wire_bytes_per_step"] - rec["wire_bytes_per_step_model"]) <= 16, rec
     assert rec["mean_loss"] == rec["mean_loss"] and 0 < rec["mean_loss"] < 20
     assert rec["comm_wait_ms"] is not None and rec["peak_hbm_gb_per_rank"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("comm", ["compute", "fp32"])
+def test_emulated_ddp_numerics_track_world1(comm):
+    """Identical-ranks semantics: under emulate:8 an all-reduce returns 8x the bucket (what 8 ranks
+    holding this rank's gradient would sum) and DDP divides by 8, so an emulated DDP run must train
+    like the world-1 run (same losses within bf16 noise).  This drives the sparse token-row
+    exchange of the tied embedding (all-gather of rows + ids, scatter-add into the reduced bf16 or
+    fp32 buffer).  (The sharded engines cannot: other ranks' shards are never updated here.)"""
+    common = ["--steps", "8", "--warmup", "4", "--seq-len", "512", "--strategy", "ddp", "--dtype", "bf16",
+              "--grad-comm-dtype", comm, "--graphs", "off"]
+    w1 = _bench(common)
+    e8 = _bench(common + ["--emulate", "8"])
+    assert abs(w1["mean_loss"] - e8["mean_loss"]) < 2e-3 * w1["mean_loss"], (w1["mean_loss"], e8["mean_loss"])
+    assert abs(w1["final_loss"] - e8["final_loss"]) < 5e-3 * w1["final_loss"], (w1["final_loss"], e8["final_loss"])
