@@ -4,7 +4,7 @@
 // A real RCCL collective on an 8 x MI355X node is a kernel of `channels` workgroups that, for the
 // collective's duration, occupies those CUs and streams the buffer through HBM while the bytes cross
 // xGMI.  This kernel reproduces exactly those three things for the compute that runs beside it:
-//   * occupancy: `channels` workgroups of 256 threads stay resident until the modelled end time;
+//   * occupancy: `channels` workgroups of 512 threads stay resident until the modelled end time;
 //   * HBM traffic: it reads the collective's buffer (`traffic`, `passes` times) and writes the
 //     stand-in result;
 //   * duration: every wave paces itself against the 100 MHz constant wall clock so that its share
@@ -25,7 +25,7 @@
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;
 
 struct EmuArgs {
   const uint4* traffic;   // buffer streamed to model the collective's HBM reads
@@ -64,28 +64,45 @@ DLTB_DEV uint4 scaled(uint4 v, float s, int f32) {
   return pack8(f);
 }
 
+// One tile = kThreads x kVec 16-byte vectors (128 KiB): every lane has kVec independent loads in
+// flight before it consumes any, so 32 workgroups can stream the buffer well above the modelled
+// fabric rate and the pace, not the loop, sets the duration (measured: tests/test_emulate_gpu.py).
+constexpr int kVec = 16;
+constexpr long kTile = (long)kThreads * kVec;
+
 __global__ __launch_bounds__(kThreads) void comm_emu_kernel(EmuArgs a) {
   const uint64_t t0 = now();
-  const long num_tiles = (a.n_vec * a.replicas + kThreads - 1) / kThreads;
-  const long trf_tiles = (a.traffic_vec * a.passes + kThreads - 1) / kThreads;
-  const long tiles = num_tiles + trf_tiles;
+  const long n_num = a.n_vec * a.replicas, n_trf = a.traffic_vec * a.passes;
+  const long num_tiles = (n_num + kTile - 1) / kTile;
+  const long tiles = num_tiles + (n_trf + kTile - 1) / kTile;
   const long G = gridDim.x;
   const long mine = tiles > blockIdx.x ? (tiles - blockIdx.x + G - 1) / G : 0;
   uint32_t acc = 0;
   long k = 0;
   for (long t = blockIdx.x; t < tiles; t += G, ++k) {
     if (t < num_tiles) {
-      const long e = t * kThreads + threadIdx.x;            // element vector over (replica, j)
-      if (e < a.n_vec * a.replicas) {
-        const long r = e / a.n_vec, j = e - r * a.n_vec;
-        a.dst[r * a.rep_stride_vec + j] = scaled(a.src[j], a.scale, a.f32);
+      uint4 v[kVec];
+      long e[kVec];
+#pragma unroll
+      for (int u = 0; u < kVec; ++u) {                      // element vectors over (replica, j)
+        e[u] = t * kTile + u * kThreads + threadIdx.x;
+        if (e[u] < n_num) v[u] = a.src[e[u] % a.n_vec];
       }
+#pragma unroll
+      for (int u = 0; u < kVec; ++u)
+        if (e[u] < n_num) {
+          const long r = e[u] / a.n_vec, j = e[u] - r * a.n_vec;
+          a.dst[r * a.rep_stride_vec + j] = scaled(v[u], a.scale, a.f32);
+        }
     } else {
-      const long e = (t - num_tiles) * kThreads + threadIdx.x;
-      if (e < a.traffic_vec * a.passes) {
-        const uint4 v = a.traffic[e % a.traffic_vec];
-        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+      uint4 v[kVec];
+#pragma unroll
+      for (int u = 0; u < kVec; ++u) {
+        const long e = (t - num_tiles) * kTile + u * kThreads + threadIdx.x;
+        v[u] = e < n_trf ? a.traffic[e % a.traffic_vec] : make_uint4(0, 0, 0, 0);
       }
+#pragma unroll
+      for (int u = 0; u < kVec; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
     // the modelled time at which this workgroup's first k + 1 tiles are done
     pace_until(t0 + a.alpha_ticks + (uint64_t)((double)a.beta_ticks * (double)(k + 1) / (double)mine));

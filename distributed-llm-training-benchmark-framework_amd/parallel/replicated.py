@@ -132,7 +132,9 @@ class ReplicatedEngine(Engine):
         # column sums of ALL blocks are reduced by one or two colreduce_multi launches at its end
         # instead of one launch per block, and the QKV-bias partials of block i ride along with
         # block i-1's dropout colpart launch instead of a launch of their own
-        self._red = F_.GradReducer(64, defer_plain=True) if (self.world == 1 and dev.type == "cuda") else None
+        # (world > 1: the shared reducer is flushed right before each bucket's collective, so one
+        # or two colreduce launches serve a 4-block bucket instead of one per block)
+        self._red = F_.GradReducer(64, defer_plain=True) if dev.type == "cuda" else None
         # buckets are reduced strictly in bucket order (torch DDP's Reducer does the same): every
         # rank must issue its collectives in one sequence, and a unit that does not report on some
         # rank (an unused parameter) would otherwise reorder that rank's sequence
@@ -210,6 +212,8 @@ class ReplicatedEngine(Engine):
             while self._next < len(self._pending) and self._pending[self._next] == 0:
                 nb = self._next
                 self._wq.flush(self.layout.buckets[nb].units)   # this bucket's dW, then its collective
+                if self._red is not None:
+                    self._red.flush()                           # ... and its column sums
                 self._launch(nb)
                 self._next += 1
         # (micro-steps without a collective -- inside a ZeRO-1 / window-reduced accumulation
@@ -304,7 +308,8 @@ class ReplicatedEngine(Engine):
             self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g)
 
     def _drain_bucket(self, b):
-        """Wait for bucket ``b``'s reduce-scatter and add its chunk into the fp32 accumulator."""
+        """Wait for bucket ``b``'s reduce-scatter and add its chunk into the fp32 accumulator (then
+        the token rows exchanged for the tied table, when this is its bucket)."""
         w, first = self._rs_inflight.pop(b)
         w.wait()
         bk = self.layout.buckets[b]
@@ -316,6 +321,8 @@ class ReplicatedEngine(Engine):
             a.copy_(r)
         else:
             a += r
+        if self._sparse is not None and self._bucket_of[id(self._sparse[0][0])] == b:
+            self._apply_sparse()
 
     def _drain_all(self):
         for b in sorted(self._rs_inflight):
@@ -336,11 +343,14 @@ class ReplicatedEngine(Engine):
                 self._launch(b)
         self._phase("comm_wait_begin")
         self._wait_works()
-        if self._sparse is not None:
+        if self._sparse is not None and not (self._tail_defer and not self._is_boundary):
             b = self._bucket_of[id(self._sparse[0][0])]
             if b in self._rs_inflight:
-                self._drain_bucket(b)          # the token table's chunk first, then its sparse rows
-            self._apply_sparse()
+                self._drain_bucket(b)          # the token table's chunk, then its sparse rows
+            if self._sparse is not None:
+                self._apply_sparse()
+        # (ZeRO-2 inside a window: the row all-gathers stay in flight with the table's reduce-
+        # scatter and are applied when that bucket is drained, under the next forward)
         if self._tail_defer and self._is_boundary:
             self._drain_all()                   # the optimizer reads the window's full sum next
         self._phase("comm_wait_end")

@@ -54,6 +54,21 @@ def test_paced_kernel_duration_and_numerics(dt):
 
 
 @pytest.mark.gpu
+def test_paced_kernel_streams_faster_than_any_modelled_fabric():
+    """With no pacing (alpha = beta = 0) the 32 default workgroups must read a bucket far faster
+    than the modelled fabric moves it, so the modelled time -- not the kernel's own streaming --
+    sets an emulated collective's duration."""
+    dev = torch.device("cuda", 0)
+    C = _ext()
+    big = torch.ones(128 << 20, device=dev, dtype=torch.bfloat16)          # 256 MiB
+    C.comm_emu(big, 1, None, None, 1.0, 1, 0, 0.0, 0.0, 32)
+    ms = min(_time_ms(lambda: C.comm_emu(big, 1, None, None, 1.0, 1, 0, 0.0, 0.0, 32), dev) for _ in range(3))
+    gbps = big.numel() * 2 / (ms * 1e-3) / 1e9
+    print(f"[emulate] 32-workgroup unpaced read: {gbps:.0f} GB/s")
+    assert gbps > 1200.0, gbps
+
+
+@pytest.mark.gpu
 def test_emulated_collective_overlaps_compute(monkeypatch):
     monkeypatch.setenv("DLTB_COMM", "emulate:8")
     monkeypatch.setenv("DLTB_EMU_ALPHA_US", "1000")                  # a 1 ms collective
@@ -100,21 +115,49 @@ def test_bench_emulate4_wire_bytes(extra):
     rec = _bench(["--emulate", "4", "--steps", "8", "--warmup", "4", "--seq-len", "512", *extra])
     assert rec["prediction"] and rec["emulated_world"] == 4
     assert abs(rec["wire_bytes_per_step"] - rec["wire_bytes_per_step_model"]) <= 16, rec
-    assert rec["mean_loss"] == rec["mean_loss"] and 0 < rec["mean_loss"] < 20
+    # (sharded engines train on replicated shards of rank 0 -- the stand-in has no other ranks'
+    # shards -- so only finiteness is meaningful there; DDP's numerics: the test below)
+    assert rec["mean_loss"] == rec["mean_loss"] and 0 < rec["mean_loss"] < 1e4
     assert rec["comm_wait_ms"] is not None and rec["peak_hbm_gb_per_rank"] > 0
+
+
+def _train_losses(comm, steps=8):
+    from dltb.models import build_model, get_model_config
+    from dltb.parallel import engine_config, make_engine
+    torch.manual_seed(0)
+    cfg = get_model_config("A", 256)
+    cfg.n_layer = 2
+    dev = torch.device("cuda", 0)
+    with torch.device(dev):
+        model = build_model(cfg)
+    ec = engine_config("ddp", 1, "reference", bucket_mb=16.0)
+    ec.lr = 1e-3
+    ec.extra["grad_comm_dtype"] = comm
+    eng = make_engine(model, ec, dev)
+    eng.train()
+    g = torch.Generator().manual_seed(5)
+    out = []
+    for _ in range(steps):
+        x = torch.randint(0, cfg.vocab_size, (1, 256), generator=g).to(dev)
+        loss = eng(x, x)[1]
+        eng.backward(loss)
+        eng.step()
+        out.append(float(loss.item()))
+    return out
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("comm", ["compute", "fp32"])
-def test_emulated_ddp_numerics_track_world1(comm):
+def test_emulated_ddp_numerics_track_world1(comm, monkeypatch):
     """Identical-ranks semantics: under emulate:8 an all-reduce returns 8x the bucket (what 8 ranks
-    holding this rank's gradient would sum) and DDP divides by 8, so an emulated DDP run must train
-    like the world-1 run (same losses within bf16 noise).  This drives the sparse token-row
-    exchange of the tied embedding (all-gather of rows + ids, scatter-add into the reduced bf16 or
-    fp32 buffer).  (The sharded engines cannot: other ranks' shards are never updated here.)"""
-    common = ["--steps", "8", "--warmup", "4", "--seq-len", "512", "--strategy", "ddp", "--dtype", "bf16",
-              "--grad-comm-dtype", comm, "--graphs", "off"]
-    w1 = _bench(common)
-    e8 = _bench(common + ["--emulate", "8"])
-    assert abs(w1["mean_loss"] - e8["mean_loss"]) < 2e-3 * w1["mean_loss"], (w1["mean_loss"], e8["mean_loss"])
-    assert abs(w1["final_loss"] - e8["final_loss"]) < 5e-3 * w1["final_loss"], (w1["final_loss"], e8["final_loss"])
+    holding this rank's gradient would sum) and DDP divides by 8, so on the same batches an emulated
+    DDP run must train like the world-1 run (loss curves within bf16 noise).  This drives the sparse
+    token-row exchange of the tied embedding (all-gather of rows + ids, scatter-add into the reduced
+    bf16 or fp32 buffer).  (The sharded engines cannot: other ranks' shards are never updated.)"""
+    monkeypatch.delenv("DLTB_COMM", raising=False)
+    w1 = _train_losses(comm)
+    monkeypatch.setenv("DLTB_COMM", "emulate:8")
+    e8 = _train_losses(comm)
+    assert w1[0] == e8[0]                                     # same init, same first batch
+    for a, b in zip(w1, e8):
+        assert abs(a - b) < 3e-3 * a, (w1, e8)
