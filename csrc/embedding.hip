@@ -96,14 +96,14 @@ __global__ __launch_bounds__(256) void embed_bwd_pos_kernel(
 // position of each run of equal ids sums the run and adds it to dwte[id].
 __global__ __launch_bounds__(256) void embed_bwd_tok_kernel(
     const bf16_t* __restrict__ dx, const int64_t* __restrict__ sorted_ids,
-    const int64_t* __restrict__ perm, bf16_t* __restrict__ dwte, int N, int d, uint32_t thr16,
+    const int64_t* __restrict__ perm, bf16_t* __restrict__ dwte, int N, int d, long V, uint32_t thr16,
     float scale, const int64_t* __restrict__ seed_ptr, int64_t site) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N) return;
   const long id = sorted_ids[i];
   if (i > 0 && sorted_ids[i - 1] == id) return;
-  if (id < 0) return;   // ignore_index style padding ids
+  if (id < 0 || id >= V) return;   // ignore_index style padding ids; never a row outside the table
   int j_end = i + 1;
   while (j_end < N && sorted_ids[j_end] == id) ++j_end;
   const uint64_t seed = thr16 ? site_seed(seed_ptr, site) : 0ull;
@@ -131,12 +131,12 @@ constexpr int kScanMaxChunks = 8;     // d <= 8 x 512 = 4096
 
 __global__ __launch_bounds__(256) void embed_bwd_tok_scan_kernel(
     const bf16_t* __restrict__ dx, const int64_t* __restrict__ ids, bf16_t* __restrict__ dwte, int N,
-    int d, uint32_t thr16, float scale, const int64_t* __restrict__ seed_ptr, int64_t site) {
+    int d, long V, uint32_t thr16, float scale, const int64_t* __restrict__ seed_ptr, int64_t site) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= N) return;
   const long id = ids[i];
-  if (id < 0) return;
+  if (id < 0 || id >= V) return;
   DLTB_DCHECK(d % 8 == 0 && d <= kScanMaxChunks * 512);
   for (int base = 0; base < i; base += 64) {            // an earlier duplicate owns this id
     const int j = base + lane;
@@ -177,12 +177,12 @@ __global__ __launch_bounds__(256) void embed_bwd_tok_scan_kernel(
 
 }  // namespace
 
-bool dltb_embed_bwd_tok_scan(const void* dx, const int64_t* ids, void* dwte, int N, int d,
+bool dltb_embed_bwd_tok_scan(const void* dx, const int64_t* ids, void* dwte, int N, int d, long V,
                              uint32_t thr16, float scale, const int64_t* seed, int64_t site,
                              hipStream_t st) {
   if (N > kScanMaxRows || d > kScanMaxChunks * 512 || d % 8) return false;
   hipLaunchKernelGGL(embed_bwd_tok_scan_kernel, dim3(cdiv(N, 4)), dim3(256), 0, st,
-                     (const bf16_t*)dx, ids, (bf16_t*)dwte, N, d, thr16, scale, seed, site);
+                     (const bf16_t*)dx, ids, (bf16_t*)dwte, N, d, V, thr16, scale, seed, site);
   return true;
 }
 
@@ -203,9 +203,9 @@ void dltb_embed_bwd_pos(const void* dx, void* dwpe, int B, int T, int P, int d, 
 }
 
 void dltb_embed_bwd_tok(const void* dx, const int64_t* sorted_ids, const int64_t* perm,
-                        void* dwte, int N, int d, uint32_t thr16, float scale,
+                        void* dwte, int N, int d, long V, uint32_t thr16, float scale,
                         const int64_t* seed, int64_t site, hipStream_t st) {
   hipLaunchKernelGGL(embed_bwd_tok_kernel, dim3(cdiv(N, 4)), dim3(256), 0, st,
-                     (const bf16_t*)dx, sorted_ids, perm, (bf16_t*)dwte, N, d, thr16, scale, seed,
+                     (const bf16_t*)dx, sorted_ids, perm, (bf16_t*)dwte, N, d, V, thr16, scale, seed,
                      site);
 }

@@ -66,11 +66,11 @@ void dltb_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* 
 void dltb_embed_bwd_pos(const void* dx, void* dwpe, int B, int T, int P, int d, int accumulate,
                         uint32_t thr16, float scale, const int64_t* seed, int64_t site,
                         hipStream_t st);
-bool dltb_embed_bwd_tok_scan(const void* dx, const int64_t* ids, void* dwte, int N, int d,
+bool dltb_embed_bwd_tok_scan(const void* dx, const int64_t* ids, void* dwte, int N, int d, long V,
                              uint32_t thr16, float scale, const int64_t* seed, int64_t site,
                              hipStream_t st);
 void dltb_embed_bwd_tok(const void* dx, const int64_t* sorted_ids, const int64_t* perm,
-                        void* dwte, int N, int d, uint32_t thr16, float scale,
+                        void* dwte, int N, int d, long V, uint32_t thr16, float scale,
                         const int64_t* seed, int64_t site, hipStream_t st);
 
 // xent.hip

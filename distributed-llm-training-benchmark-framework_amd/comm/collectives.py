@@ -258,6 +258,9 @@ class Comm:
             self._emu_stream.wait_stream(torch.cuda.current_stream(out.device))
             with torch.cuda.stream(self._emu_stream):
                 out.view(self.world, n).copy_(inp.reshape(1, n).expand(self.world, n))
+            # the caller may free ``inp`` right away: its memory must not be handed to later work
+            # on the compute stream before this copy has read it
+            inp.record_stream(self._emu_stream)
             return self._emu("all_gather", out, async_op=async_op, track=track)
         return self._emu("all_gather", out, out.view(-1), inp.reshape(-1), 1.0, self.world, n,
                          async_op=async_op, track=track)

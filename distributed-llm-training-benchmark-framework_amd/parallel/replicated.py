@@ -42,6 +42,9 @@ from .flat import ALIGN, owner_segments, plan_layout
 from .wgrad import WgradQueue
 
 
+_SPARSE_DEFER = os.environ.get("DLTB_SPARSE_DEFER", "1") == "1"
+
+
 class ReplicatedEngine(Engine):
     name = "ddp"
     grad_write_ahead = True      # every gradient slot is a view of the flat buffer from the start
@@ -134,7 +137,8 @@ class ReplicatedEngine(Engine):
         # block i-1's dropout colpart launch instead of a launch of their own
         # (world > 1: the shared reducer is flushed right before each bucket's collective, so one
         # or two colreduce launches serve a 4-block bucket instead of one per block)
-        self._red = F_.GradReducer(64, defer_plain=True) if dev.type == "cuda" else None
+        self._red = F_.GradReducer(64, defer_plain=True) if (
+            dev.type == "cuda" and (self.world == 1 or os.environ.get("DLTB_SHARED_RED", "1") == "1")) else None
         # buckets are reduced strictly in bucket order (torch DDP's Reducer does the same): every
         # rank must issue its collectives in one sequence, and a unit that does not report on some
         # rank (an unused parameter) would otherwise reorder that rank's sequence
@@ -343,7 +347,7 @@ class ReplicatedEngine(Engine):
                 self._launch(b)
         self._phase("comm_wait_begin")
         self._wait_works()
-        if self._sparse is not None and not (self._tail_defer and not self._is_boundary):
+        if self._sparse is not None and not (self._tail_defer and not self._is_boundary and _SPARSE_DEFER):
             b = self._bucket_of[id(self._sparse[0][0])]
             if b in self._rs_inflight:
                 self._drain_bucket(b)          # the token table's chunk, then its sparse rows
