@@ -220,6 +220,47 @@ int dltb_blaslt_run(const BltProblem& p, const void* A, const void* B, void* C, 
   return it->second.first->run(st) == HIPBLAS_STATUS_SUCCESS ? 0 : -5;
 }
 
+// Untuned problems: hipBLASLt's own heuristic choice (its first suggestion, the one torch's
+// matmul would also get without TunableOp), initialised once per (problem, pointers, stream) in
+// the same LRU cache, so an untuned product -- an fp16 GEMM of the reference-precision DDP/FSDP
+// runs, an unbatched weight gradient of a multi-rank step -- is also a bare launch after its first
+// call instead of ~25 us of torch-dispatch host time.  The heuristic's pick per problem SHAPE is
+// memoised too, so new operand pointers cost one initialise, not another heuristic query.
+int dltb_blaslt_run_heuristic(const BltProblem& p, const void* A, const void* B, void* C, const void* bias,
+                              hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  static std::map<Key, hipblasLtMatmulAlgo_t> picks;     // shape key (null pointers) -> algo
+  auto& c = cache();
+  const Key key = key_of(p, -1, 0, 0, A, B, C, bias, st);
+  auto it = c.map.find(key);
+  if (it == c.map.end()) {
+    auto g = make_gemm(p, A, B, C, bias);
+    if (!g) return -2;
+    const Key shape = key_of(p, -1, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+    auto pk = picks.find(shape);
+    if (pk == picks.end()) {
+      hipblaslt_ext::GemmPreference pref;
+      pref.setMaxWorkspaceBytes(kWorkspace);
+      std::vector<hipblasLtMatmulHeuristicResult_t> r;
+      if (g->algoGetHeuristic(1, pref, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) return -1;
+      pk = picks.emplace(shape, r[0].algo).first;
+    }
+    auto t = tuning_of(0, 0);
+    size_t need = 0;
+    if (g->isAlgoSupported(pk->second, t, need) != HIPBLAS_STATUS_SUCCESS || need > kWorkspace) return -3;
+    if (g->initialize(pk->second, t, workspace(st), true, st) != HIPBLAS_STATUS_SUCCESS) return -4;
+    if (c.map.size() >= kMaxCached) {
+      c.map.erase(c.order.back());
+      c.order.pop_back();
+    }
+    c.order.push_front(key);
+    it = c.map.emplace(key, std::make_pair(std::move(g), c.order.begin())).first;
+  } else if (it->second.second != c.order.begin()) {
+    c.order.splice(c.order.begin(), c.order, it->second.second);
+  }
+  return it->second.first->run(st) == HIPBLAS_STATUS_SUCCESS ? 0 : -5;
+}
+
 std::string dltb_blaslt_name(int algo) {
   std::lock_guard<std::mutex> lk(g_mu);
   hipblasLtMatmulAlgo_t a;

@@ -43,5 +43,9 @@ std::vector<BltResult> dltb_blaslt_sweep(const BltProblem& p, const void* A, con
 int dltb_blaslt_run(const BltProblem& p, const void* A, const void* B, void* C, const void* bias, int algo,
                     int splitk, int wgm, hipStream_t st);
 
+// D (+)= A B with hipBLASLt's heuristic solution for an untuned problem (memoised per shape).
+int dltb_blaslt_run_heuristic(const BltProblem& p, const void* A, const void* B, void* C, const void* bias,
+                              hipStream_t st);
+
 // Solution name of an algo index (validation of stored tables against the loaded library).
 std::string dltb_blaslt_name(int algo);

@@ -63,11 +63,15 @@ def main():
         h2 = (time.perf_counter() - t0) / 2
         torch.cuda.synchronize()
         print(f"host-only cost (GPU busy ahead): {h2 * 1e3:.3f} ms/step")
+    # the backward Functions run on autograd's device thread, which cProfile does not see: run the
+    # profiled steps with autograd on the calling thread
+    torch.autograd.set_multithreading_enabled(False)
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(a.steps):
         step()
     pr.disable()
+    torch.autograd.set_multithreading_enabled(True)
     torch.cuda.synchronize()
     s = io.StringIO()
     pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(a.top)
