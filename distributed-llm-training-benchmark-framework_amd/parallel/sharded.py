@@ -174,6 +174,13 @@ class ShardedEngine(Engine):
         nparam = sum(u.numel for u in self.model.units())
         self._cache_wt = (self.world == 1 and self.accum > 1 and nparam < 2_000_000_000
                           and bool(cfg.extra.get("cache_weight_t", True)))
+        # world > 1: the gathered W is a transient buffer, so the cache keeps its own transposed copy,
+        # made the first time a unit's backward needs it in an accumulation window (the parameters
+        # do not change inside a window) and reused by the window's other micro-steps -- one LDS
+        # transpose per matrix per window buys the NT-form data-gradient GEMMs.  Same policy as
+        # world 1 (windows, models below 2B parameters: the copy is a full model's worth of W^T)
+        self._wt_multi = {} if (self.world > 1 and self.accum > 1 and nparam < 2_000_000_000
+                                and dev.type == "cuda" and bool(cfg.extra.get("cache_weight_t", True))) else None
         if self.world > 1:
             # modelled wire bytes one rank sends per micro-step (ring algorithms), per group: its
             # all-gathers (once per optimizer step when everything stays gathered; once per
@@ -194,6 +201,20 @@ class ShardedEngine(Engine):
                 per += frac * g.total * e * (ng + 1.0)
             per += frac * p_total * e * (1.0 + 1.0 / self.accum)
             self.comm_bytes_per_step = int(per)
+
+    def weight_t(self, unit, i, w):
+        if self._wt_multi is None:
+            return super().weight_t(unit, i, w)
+        if w.dim() != 2 or not w.is_cuda:
+            return None
+        key = (unit.index, i)
+        ent = self._wt_multi.get(key)
+        if ent is None:
+            ent = self._wt_multi[key] = [torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device), -1]
+        if ent[1] != self.opt_steps:           # first use in this window: transpose the gathered W
+            ext().transpose_into(w, ent[0])
+            ent[1] = self.opt_steps
+        return ent[0]
 
     def _slot_key(self, unit, i):
         """(buffer, element offset) of gradient slot ``i`` of ``unit`` at world size 1."""
@@ -450,6 +471,9 @@ class ShardedEngine(Engine):
 
     def _after_param_load(self):
         self._wt_epoch = -1                       # cached transposes are stale
+        if self._wt_multi:
+            for ent in self._wt_multi.values():
+                ent[1] = -1
         for grp in self.groups:                   # gathered copies (if any) are stale
             self._release(grp)
         pc = self.p_layout.owner_numel

@@ -74,7 +74,7 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "emulated_scaling.txt"))
     ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
-    ap.add_argument("--strategies", nargs="+", default=list(STRATS))
+    ap.add_argument("--strategies", nargs="*", default=list(STRATS))
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--m7b", action="store_true", help="also Mistral-7B-shape ZeRO-3 at N = 8 (BASELINE config #5)")
