@@ -22,6 +22,7 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
+import os
 from types import SimpleNamespace
 
 import torch
@@ -81,8 +82,10 @@ class _EmbedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, idx, model):
         rt, unit = model.rt, model.unit_embed
-        wte = rt.acquire_tied(model.unit_head)[2]
-        (wpe,) = rt.acquire(unit)
+        (tu, ti), (_, pi) = model.tok_slot, model.pos_slot
+        own = rt.acquire(unit)
+        wpe = own[pi]
+        wte = own[ti] if tu is unit else rt.acquire_tied(tu)[ti]
         p = model.drop_p
         x = F_.embed_fwd(idx, wte, wpe, p, rt.seed, model.site_embed)
         rt.release_forward(unit)
@@ -94,7 +97,7 @@ class _EmbedFn(torch.autograd.Function):
         model = ctx.model
         rt, unit = model.rt, model.unit_embed
         rt.acquire_backward(unit)
-        rt.embedding_backward((model.unit_head, 2), (unit, 0), dx.contiguous(), ctx.idx, model.drop_p, rt.seed,
+        rt.embedding_backward(model.tok_slot, model.pos_slot, dx.contiguous(), ctx.idx, model.drop_p, rt.seed,
                               model.site_embed)
         rt.grads_ready(unit)
         rt.release_backward(unit)
@@ -210,7 +213,10 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_in, m_in, model, targets, return_logits):
         rt = model.rt
-        lnw, lnb, wte = rt.acquire(model.unit_head)
+        tu, ti = model.tok_slot
+        hp = rt.acquire(model.unit_head)
+        lnw, lnb = hp[0], hp[1]
+        wte = hp[ti] if tu is model.unit_head else rt.acquire_tied(tu)[ti]
         if m_in is None:
             x = x_in
             _, h, mean, rstd = F_.norm_fwd(x, None, lnw, lnb, LN_EPS, False)
@@ -243,11 +249,14 @@ class _HeadFn(torch.autograd.Function):
         rt = model.rt
         (x, h, mean, rstd, dl, count) = ctx.saved
         ctx.saved = None
-        lnw, lnb, wte = rt.acquire_backward(model.unit_head)
-        dw, acc_w = rt.grad_slot(model.unit_head, 2)             # tied lm_head / wte (dense part)
+        tu, ti = model.tok_slot
+        hp = rt.acquire_backward(model.unit_head)
+        lnw, lnb = hp[0], hp[1]
+        wte = hp[ti] if tu is model.unit_head else rt.acquire_tied(tu)[ti]
+        dw, acc_w = rt.grad_slot(tu, ti)                          # tied lm_head / wte (dense part)
         hs, g = F_.scale_by(h, dloss, count)                      # g = dloss / count (device)
         F_.linear_wgrad(dl, hs, dw, None, acc_w)
-        dh = F_.head_dgrad(dl, wte, rt.weight_t(model.unit_head, 2, wte), g)
+        dh = F_.head_dgrad(dl, wte, rt.weight_t(tu, ti, wte), g)
         gw, acc = rt.grad_slot(model.unit_head, 0)
         gb, _ = rt.grad_slot(model.unit_head, 1)
         dx = F_.norm_bwd(dh, x, lnw, mean, rstd, None, gw, gb, acc, False)
@@ -299,13 +308,20 @@ class TinyGPT(nn.Module):
     def _build_units(self):
         t = self.transformer
         # the tied token table (wte = lm_head.weight) is the head unit's third parameter: the head's
-        # backward, the first of the step, completes its dense gradient (see _EmbedFn)
-        self.unit_embed = Unit("embed", [("transformer.wpe.weight", t["wpe"].weight)], 0)
+        # backward, the first of the step, completes its dense gradient (see _EmbedFn).
+        # DLTB_TIE_IN_HEAD=0 (A/B only) keeps it in the embedding unit, reduced after the last
+        # backward op as before round 3.
+        tie_in_head = os.environ.get("DLTB_TIE_IN_HEAD", "1") == "1"
+        wpe = [("transformer.wpe.weight", t["wpe"].weight)]
+        wte = [("transformer.wte.weight", t["wte"].weight)]
+        self.unit_embed = Unit("embed", wpe if tie_in_head else wte + wpe, 0)
         self.unit_blocks = [Unit(f"h.{i}", [(f"transformer.h.{i}.{n}", p) for n, p in blk.param_list()], i + 1)
                             for i, blk in enumerate(t["h"])]
         self.unit_head = Unit("head", [("transformer.ln_f.weight", t["ln_f"].weight),
-                                       ("transformer.ln_f.bias", t["ln_f"].bias),
-                                       ("transformer.wte.weight", t["wte"].weight)], len(self.unit_blocks) + 1)
+                                       ("transformer.ln_f.bias", t["ln_f"].bias)] + (wte if tie_in_head else []),
+                              len(self.unit_blocks) + 1)
+        self.tok_slot = (self.unit_head, 2) if tie_in_head else (self.unit_embed, 0)
+        self.pos_slot = (self.unit_embed, 0) if tie_in_head else (self.unit_embed, 1)
 
     def units(self):
         """Units in forward order (the engines reverse it for backward-ordered buckets)."""

@@ -12,7 +12,10 @@ then per problem:
 
 and merges the winners into the table (default configs/blaslt/blaslt_gfx950.csv).
 
-    python scripts/tune_blaslt.py --tier A --seq-len 2048 --strategy zero2 [--dtype bf16]
+    python scripts/tune_blaslt.py --tier A --seq-len 2048 --strategy zero2 [--dtype bf16] [--emulate N]
+
+``--emulate N`` records the problems of rank 0 of an N-rank job (DLTB_COMM=emulate:N): the
+per-bucket / per-unit weight gradients and the other shapes that only exist at world size > 1.
 """
 import argparse
 import csv
@@ -82,18 +85,20 @@ def record_problems(args):
     with torch.device(device):
         model = build_model(mcfg)
     h = argparse.Namespace(strategy=args.strategy, deepspeed_config=None, fsdp_config=None, grad_accum=args.grad_accum,
-                           accum_semantics="reference", dtype=args.dtype, bucket_mb=recommend_bucket_mb(1), seed=42,
+                           accum_semantics="reference", dtype=args.dtype,
+                           bucket_mb=recommend_bucket_mb(max(1, args.emulate)), seed=42,
                            grad_reduce="micro", grad_comm_dtype="compute", fsdp_wrap="block")
     engine, _ = _engine_for(h, model, device)
     ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 64, 0)
     batches = make_batcher("device", ds, 1, 1, 0, args.strategy, device)
     engine.train()
     blaslt.start_recording()
-    for _ in range(engine.accum):
+    for _ in range(engine.accum + 1):     # + 1: a window boundary, then a first micro-step again
         b = next(batches)
         loss = engine(b, b)[1]
         engine.backward(loss)
         engine.step()
+    engine.finalize()
     torch.cuda.synchronize()
     return blaslt.stop_recording(), (model, engine)
 
@@ -114,7 +119,10 @@ def main():
                          "(entries at parity still pay: a few us of host time per call instead of ~25)")
     ap.add_argument("--out", default=blaslt.DEFAULT_FILE)
     ap.add_argument("--limit", type=int, default=0, help="tune at most this many problems (0 = all)")
+    ap.add_argument("--emulate", type=int, default=0, help="record the problems of an N-rank job's rank 0")
     args = ap.parse_args()
+    if args.emulate:
+        os.environ["DLTB_COMM"] = f"emulate:{args.emulate}"
     from dltb.utils.gemm_tuning import setup_tunableop
     os.environ["DLTB_BLASLT_FILE"] = "none"          # record / compare against the torch path only
     print(f"[tune_blaslt] TunableOp: {setup_tunableop('use')}", flush=True)
