@@ -330,7 +330,7 @@ def host_enqueue_ms(one_step, k, device):
     hold_us = 3e5 + 5e4 * k
     for _ in range(2):      # the first pass grows the allocator's cache: blocks still recorded on a
         torch.cuda.synchronize(device)     # collective stream cannot be reused while the GPU is held
-        ext().comm_emu(None, 1, None, None, 1.0, 1, 0, hold_us, 0.0, 1)      # one paced wave: GPU busy
+        ext().comm_emu(None, 1, None, None, 1.0, 1, 0, hold_us, 0.0, 1, 0)   # one paced wave: GPU busy
         t0 = time.perf_counter()
         for _ in range(k):
             one_step(False)

@@ -228,15 +228,16 @@ class Comm:
         from ..ops._ext import ext
         if self._emu_stream is None:
             self._emu_stream = torch.cuda.Stream(device=full.device, priority=-1)
-        side, cur = self._emu_stream, torch.cuda.current_stream(full.device)
-        side.wait_stream(cur)                 # the collective starts after its producers
+            self._emu_handle = self._emu_stream.cuda_stream
+        side = self._emu_stream
+        side.wait_stream(torch.cuda.current_stream(full.device))   # starts after its producers
         alpha, beta = self._emu_time(op, full)
-        with torch.cuda.stream(side):
-            ext().comm_emu(full, self.emu_passes, dst, src, float(scale), int(replicas), int(rep_stride),
-                           float(alpha), float(beta), self.emu_channels)
-        keep = [t for t in (full, dst, src) if t is not None]
+        ext().comm_emu(full, self.emu_passes, dst, src, float(scale), int(replicas), int(rep_stride),
+                       float(alpha), float(beta), self.emu_channels, self._emu_handle)
+        keep = (full, dst, src)
         for t in keep:
-            t.record_stream(side)
+            if t is not None:
+                t.record_stream(side)
         ev = torch.cuda.Event()
         ev.record(side)
         w = _EmuWork(ev, keep)

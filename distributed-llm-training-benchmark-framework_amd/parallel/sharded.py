@@ -153,6 +153,7 @@ class ShardedEngine(Engine):
                                if any(self._persistent(u, i) for i in range(len(u.params)))])
         self._p_left = self._p_pending
         self._held_grads = []
+        self._view_cache = {}        # id(unit) -> (gathered buffer, parameter views into it)
         self._reduced = set()        # group ids reduce-scattered in this micro-step
         self._p_reduced = False      # the persistent block reduce-scattered in this micro-step
         self._sparse = None          # (token slot, persistent?, gathered rows, gathered ids, works)
@@ -255,6 +256,8 @@ class ShardedEngine(Engine):
     def _release(self, g):
         if self.world == 1 or g.full is None:
             return
+        for u in g.units:             # cached views keep the storage alive: drop them with it
+            self._view_cache.pop(id(u), None)
         if g.work is not None:
             g.work.wait()
             g.work = None
@@ -262,6 +265,9 @@ class ShardedEngine(Engine):
 
     def _views(self, unit):
         g = self._group_of[id(unit)]
+        hit = self._view_cache.get(id(unit))
+        if hit is not None and hit[0] is g.full:
+            return hit[1]             # same gathered buffer (keep-all, or forward -> backward of one unit)
         out = []
         for i in range(len(unit.params)):
             s = self.p_layout.slots.get((id(unit), i))
@@ -270,6 +276,7 @@ class ShardedEngine(Engine):
             else:
                 s = g.layout.slot(unit, i)
                 out.append(g.full[s.offset:s.offset + s.numel].view(s.shape))
+        self._view_cache[id(unit)] = (g.full, out)
         return out
 
     def _prefetch(self, g, direction):
