@@ -47,7 +47,8 @@ class _Group:
         self.shard = None            # this rank's bf16 chunk (view of the engine's shard buffer)
         self.full = None             # gathered full buffer (None when released)
         self.work = None             # in-flight all-gather
-        self.grad = None             # full gradient buffer of the current backward
+        self.grad = None             # full gradient buffer of the current backward (= grad_buf, or None)
+        self.grad_buf = None         # the group's gradient buffer, allocated once
         self.fwd_left = 0
         self.bwd_left = 0
         self.root = False
@@ -154,6 +155,10 @@ class ShardedEngine(Engine):
         self._p_left = self._p_pending
         self._held_grads = []
         self._view_cache = {}        # id(unit) -> (gathered buffer, parameter views into it)
+        self._gviews = {}            # (id(unit), i) -> (gradient slot view, its group or None)
+        # resident group gradient buffers at world > 1 for models below 2B parameters (a full model's
+        # worth of bf16 gradients per rank: 0.47 GB at TinyGPT-A; Mistral-7B keeps transient ones)
+        self._grad_resident = sum(u.numel for u in self.model.units()) < 2_000_000_000
         self._reduced = set()        # group ids reduce-scattered in this micro-step
         self._p_reduced = False      # the persistent block reduce-scattered in this micro-step
         self._sparse = None          # (token slot, persistent?, gathered rows, gathered ids, works)
@@ -315,19 +320,39 @@ class ShardedEngine(Engine):
         return self._views(unit)
 
     def grad_slot(self, unit, i):
-        s = self.p_layout.slots.get((id(unit), i))
+        key = (id(unit), i)
+        v = self._gviews.get(key)
+        if v is not None:
+            g = v[1]
+            if g is not None and g.grad is None:
+                g.grad = g.grad_buf
+            return v[0], self._mark(unit, i)
+        s = self.p_layout.slots.get(key)
         if s is not None:
-            return self.p_grad[s.offset:s.offset + s.numel].view(s.shape), self._mark(unit, i)
+            self._gviews[key] = (self.p_grad[s.offset:s.offset + s.numel].view(s.shape), None)
+            return self._gviews[key][0], self._mark(unit, i)
         g = self._group_of[id(unit)]
-        if g.grad is None:
-            if self.world == 1:
-                g.grad = self.rs_out[g.owner_start:g.owner_start + g.chunk]
-            else:
+        if not self._grad_resident and self.world > 1:
+            # large models: a transient full gradient buffer per group and micro-step
+            if g.grad is None:
                 g.grad = torch.empty(g.total, dtype=self.shard_buf.dtype, device=self.device)
-            # padding must be zero: it is reduced and enters the gradient norm
+                self._zero_padding(g)
+            s = g.layout.slot(unit, i)
+            return g.grad[s.offset:s.offset + s.numel].view(s.shape), self._mark(unit, i)
+        if g.grad_buf is None:
+            # ONE gradient buffer per group for the whole run (world 1: the group's owner space; world
+            # > 1: the full flat buffer its reduce-scatter reads, reused every micro-step once the
+            # previous reduce-scatter is waited -- no allocation, no padding fill, cached slot views);
+            # its padding is zeroed once (it is reduced and enters the gradient norm; nothing writes it)
+            g.grad_buf = self.rs_out[g.owner_start:g.owner_start + g.chunk] if self.world == 1 else \
+                torch.empty(g.total, dtype=self.shard_buf.dtype, device=self.device)
+            g.grad = g.grad_buf
             self._zero_padding(g)
+        if g.grad is None:
+            g.grad = g.grad_buf
         s = g.layout.slot(unit, i)
-        return g.grad[s.offset:s.offset + s.numel].view(s.shape), self._mark(unit, i)
+        self._gviews[key] = (g.grad_buf[s.offset:s.offset + s.numel].view(s.shape), g)
+        return self._gviews[key][0], self._mark(unit, i)
 
     def _zero_padding(self, g):
         cur = 0
