@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--out", default=blaslt.DEFAULT_FILE)
     ap.add_argument("--limit", type=int, default=0, help="tune at most this many problems (0 = all)")
     ap.add_argument("--emulate", type=int, default=0, help="record the problems of an N-rank job's rank 0")
+    ap.add_argument("--only-new", action="store_true", help="skip problems the table already holds")
     args = ap.parse_args()
     if args.emulate:
         os.environ["DLTB_COMM"] = f"emulate:{args.emulate}"
@@ -136,6 +137,9 @@ def main():
             for r in csv.DictReader(f):
                 rows[tuple(r[k] for k in blaslt.FIELDS[:15])] = r
     items = list(probs.items())
+    if args.only_new:
+        items = [(k, v) for k, v in items if tuple(str(x) for x in k) not in rows]
+        print(f"[tune_blaslt] {len(items)} of them not in {args.out} yet", flush=True)
     if args.limit:
         items = items[:args.limit]
     C = ext()
