@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void embed_bwd_tok_kernel(
 // position with that id in ascending order (deterministic) and adds the sum to dwte[id].  The id
 // scans read 8 * N bytes per wave from L1/L2; at N = 2048 that replaces a torch radix sort plus its
 // index bookkeeping (~35 us) by nothing.
-constexpr int kScanMaxRows = 16384;
+constexpr int kScanMaxRows = 4096;     // beyond: the sort path (the duplicate scan is O(N^2 / 64))
 constexpr int kScanMaxChunks = 8;     // d <= 8 x 512 = 4096
 
 __global__ __launch_bounds__(256) void embed_bwd_tok_scan_kernel(

@@ -232,8 +232,11 @@ class Comm:
         side = self._emu_stream
         side.wait_stream(torch.cuda.current_stream(full.device))   # starts after its producers
         alpha, beta = self._emu_time(op, full)
-        ext().comm_emu(full, self.emu_passes, dst, src, float(scale), int(replicas), int(rep_stride),
-                       float(alpha), float(beta), self.emu_channels, self._emu_handle)
+        # (DLTB_EMU_HBM_PASSES=0: no traffic stream, the numerics stand-in only -- isolates the
+        # N-rank code path from the collectives' HBM contention)
+        ext().comm_emu(full if self.emu_passes > 0 else None, max(1, self.emu_passes), dst, src, float(scale),
+                       int(replicas), int(rep_stride), float(alpha), float(beta), self.emu_channels,
+                       self._emu_handle)
         keep = (full, dst, src)
         for t in keep:
             if t is not None:
