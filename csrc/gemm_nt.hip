@@ -1,0 +1,378 @@
+// bf16 "NT" GEMM for the per-layer products of a training step (gfx950, CDNA4):
+//
+//   C[M, N] = A[M][K] . B[N][K]^T  (+ bias[n])  (+ C when accumulating)       fp32 accumulate
+//
+// Every forward product (x W^T) and every data gradient against the cached W^T (dY (W^T)^T) of a
+// TinyGPT / Mistral block has this form with M = tokens.  At M = 2048 one product's output is
+// 2-8 M elements: a 16 x 16 grid of 128 x (N/16) tiles puts exactly ONE workgroup on each of the
+// 256 CUs, and each CU must then pull (BM + BN) x K x 2 bytes of operands out of its XCD's L2.
+// Measured (scripts/probes/l2_stream_probe.hip): one workgroup per CU streams GEMM-shaped tiles at
+// 80-105 GB/s by LDS-DMA and 112-128 GB/s by plain vector loads, so these products are bound by
+// that per-CU operand stream (a 128 x 64 tile at K = 4096 is 1.57 MB per CU), not by the MFMAs.
+//
+// Structure (512 threads, one workgroup per CU, one tile per workgroup, no split-K):
+//   * waves 4-7 (loaders) fill an NSTAGE-deep LDS ring by LDS-DMA (global_load_lds_dwordx4,
+//     swizzle on the source address, mfma_tiles.h; per-lane offsets computed once, wave-uniform
+//     base advanced by SALU) -- or, with RD > 0, stage RD k-steps in VGPRs and ds_write them;
+//   * waves 0-3 (consumers, 2 x 2, v_mfma_f32_32x32x16_bf16) read a whole stage's fragments one
+//     k-step ahead into a second register set, so no MFMA waits on an LDS round trip;
+//   * one raw s_barrier per k-step with a COUNTED vmcnt on the loader side: NSTAGE-2 stages stay in
+//     flight across it (hipcc's __syncthreads would drain the ring with vmcnt(0));
+//   * an XCD-aware tile walk (workgroups b, b+8, ... share an XCD under round-robin dispatch; each
+//     XCD's 32 tiles form a gm x (32/gm) block so its A and B panels are shared in its 4 MB L2).
+// Status: parity with hipBLASLt's stream-K solutions on the N = 1024 products (0.96-1.02x) and
+// 0.8-0.9x on N = 3072 / 4096 (profiles/gemm_nt_r3.txt), so the step keeps hipBLASLt; this kernel
+// is the measured own-MFMA alternative (scripts/bench_gemm_nt.py) and its ablation builds
+// (DLTB_NT_ABL, scripts/probes/gemm_nt_abl.cpp) locate the bound.
+#include "common.h"
+#include "launchers.h"
+#include "mfma_tiles.h"
+
+#ifndef DLTB_NT_ABL
+#define DLTB_NT_ABL 0   // ablation builds (scripts/probes/gemm_nt_abl.hip): 1 no MFMA, 2 no DMA in the loop, 3 no LDS reads/MFMA
+#endif
+
+namespace {
+
+struct NtArgs {
+  const bf16_t* a;
+  const bf16_t* b;
+  bf16_t* c;
+  const bf16_t* bias;
+  long lda, ldb, ldc;
+  int M, N, K;
+  int gm;            // m-blocks per group of the tile walk
+  int accumulate;
+};
+
+template <int GLDS, int N>
+DLTB_DEV void wait_stages(int ahead) {      // vmcnt(min(ahead, N) * GLDS), compile-time immediates
+  if constexpr (N > 0) {
+    if (ahead >= N) {
+      wait_vm<N * GLDS>();
+      return;
+    }
+    wait_stages<GLDS, N - 1>(ahead);
+  } else {
+    wait_vm<0>();
+  }
+}
+
+// 512 threads: waves 0-3 (consumers) only read LDS and issue MFMAs, waves 4-7 (loaders) only issue
+// the LDS-DMA stages.  An LDS-DMA wave-instruction holds its issuing wave for ~80-100 cycles while
+// the CU's address path drains the other waves' requests, so a wave that both loads and multiplies
+// serialises the two (measured: scripts/probes/l2_stream_probe.hip, profiles/gemm_nt_r3.txt).
+//
+// Consumers read a whole stage's fragments one k-step AHEAD (two named register sets, the k-loop
+// unrolled by two), so the MFMAs of stage kt never wait on an LDS round trip; the one s_barrier per
+// k-step therefore certifies stage kt+1 (loaders wait for it) and frees stage kt's slot (consumers
+// drained their reads of it with lgkmcnt(0)), and the loaders refill that slot with stage
+// kt + NSTAGE right after the barrier: NSTAGE-2 stages stay in flight across every barrier.
+template <int BM, int BN, int BK>
+struct NtGeo {
+  static constexpr int WM = BM / 2, WN = BN / 2;        // consumer wave sub-tile (2 x 2 waves)
+  static constexpr int FM = WM / 32, FN = WN / 32;      // 32 x 32 MFMA tiles per wave
+  static constexpr int KS = BK / 16;                    // k16 MFMA steps per stage
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+};
+
+template <int BM, int BN, int BK>
+struct NtFrags {
+  using G = NtGeo<BM, BN, BK>;
+  bfx8 a[G::KS][G::FM], b[G::KS][G::FN];
+  DLTB_DEV void read(const char* sa, int wm, int wn, int r, int h) {
+    if constexpr (DLTB_NT_ABL == 3) return;
+    const char* sb = sa + G::A_BYTES;
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s) {
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i) a[s][i] = row_frag<BK>(sa, wm * G::WM + 32 * i + r, 2 * s + h);
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j) b[s][j] = row_frag<BK>(sb, wn * G::WN + 32 * j + r, 2 * s + h);
+    }
+  }
+  DLTB_DEV void mma(f32x16 (&acc)[G::FM][G::FN]) const {
+    if constexpr (DLTB_NT_ABL == 1 || DLTB_NT_ABL == 3) {
+#pragma unroll
+      for (int s = 0; s < G::KS; ++s) {
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) asm volatile("" ::"v"(a[s][i]));
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) asm volatile("" ::"v"(b[s][j]));
+      }
+      return;
+    }
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s)
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) acc[i][j] = mfma32(b[s][j], a[s][i], acc[i][j]);   // lane <-> m
+  }
+};
+
+// Retire this wave's LDS reads (the next fragment set) before the barrier that lets the loaders
+// refill their slot.  The builtin (not inline asm) so that hipcc's waitcnt pass sees the fragments
+// as ready and does not re-wait for them behind the NEXT set's reads; the scheduling fences keep
+// the preceding MFMAs in front of it.
+DLTB_DEV void drain_lds_reads() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt((15) | (3 << 14) | (7 << 4) | (0 << 8));   // lgkmcnt(0) only
+  __builtin_amdgcn_sched_barrier(0);
+}
+// s_barrier that LDS reads cannot cross: the builtin alone is no memory fence to the compiler, which
+// would otherwise sink (or re-issue) a fragment read past the barrier that lets its slot be refilled
+DLTB_DEV void nt_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// RD > 0: register-staged loaders instead of LDS-DMA.  Each loader wave keeps RD stages of its
+// share in VGPRs (global_load_dwordx4, up to RD stages in flight without holding LDS) and writes a
+// stage into the LDS ring (ds_write_b128, the same lane-linear swizzled image the DMA would produce)
+// two k-steps before the consumers read it; the ring then needs only NSTAGE = 3 slots.  Plain vector
+// loads stream 120-128 GB/s per CU from L2 against 80-105 for LDS-DMA
+// (scripts/probes/l2_stream_probe.hip).
+template <int BM, int BN, int BK, int NSTAGE, int RD>
+__global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
+  using G = NtGeo<BM, BN, BK>;
+  using TA = GldsTile<BK, BM, true>;
+  using TB = GldsTile<BK, BN, true>;
+  constexpr int GLDS = TA::NI + TB::NI;          // LDS-DMA wave-instructions per stage per loader wave
+  static_assert(GLDS * (NSTAGE - 1) < 64, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wave >= 4;
+  const int wv = wave & 3;                       // consumer sub-tile / loader share
+  const int wm = wv & 1, wn = wv >> 1;
+
+  // ---- tile walk: XCD-major, then groups of gm m-blocks x all n-blocks
+  const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  int mb, nb;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {
+    const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  } else {
+    mb = idx / tiles_n;
+    nb = idx - mb * tiles_n;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = g.K / BK;                       // even (host check)
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * BK == g.K && nk >= 2 && (nk & 1) == 0);
+
+  if (RD > 0 && loader) {
+    // ======================= loader waves: register-staged ring =======================
+    constexpr int NA = TA::NI, NB = TB::NI, NI = NA + NB, D = RD > 0 ? RD : 1;
+    uint32_t offA[NA], offB[NB];
+    TA::offsets(g.lda, wv, lane, offA);
+    TB::offsets(g.ldb, wv, lane, offB);
+    const char* pa = (const char*)(g.a + (long)m0 * g.lda);
+    const char* pb = (const char*)(g.b + (long)n0 * g.ldb);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 R[D][NI];
+    auto gload = [&](int stage, u32x4 (&r)[NI]) {
+      const char* ba = pa + stage * (BK * 2);
+      const char* bb = pb + stage * (BK * 2);
+#pragma unroll
+      for (int i = 0; i < NA; ++i) r[i] = *reinterpret_cast<const u32x4*>(ba + offA[i]);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) r[NA + i] = *reinterpret_cast<const u32x4*>(bb + offB[i]);
+    };
+    auto swrite = [&](int stage, const u32x4 (&r)[NI]) {
+      char* sa = smem + (stage % NSTAGE) * G::STAGE + lane * 16;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4*>(sa + (wv * NA + i) * 1024) = r[i];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) *reinterpret_cast<u32x4*>(sa + G::A_BYTES + (wv * NB + i) * 1024) = r[NA + i];
+    };
+    // (no conditional loads or stores: a register array assigned under a run-time condition is kept
+    // in scratch.  Past the last stage the loads re-read stage nk-1 and the stores fill a slot no
+    // consumer reads again; nk is a multiple of D.)
+#pragma unroll
+    for (int d = 0; d < D; ++d) gload(d, R[d]);
+    // stages 0 and 1 into LDS before B_init (B_init: stage 0 ready, B_0: stage 1 ready)
+    swrite(0, R[0]);
+    gload(min(D, nk - 1), R[0]);
+    swrite(1, R[1 % D]);
+    gload(min(D + 1, nk - 1), R[1 % D]);
+    drain_lds_reads();                           // (lgkmcnt(0): the ds_writes have landed)
+    nt_barrier();                                // B_init
+    for (int kb = 0; kb < nk; kb += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int kt = kb + u;
+        nt_barrier();                            // B_kt
+        const int j = kt + 2;                    // stage written now; its slot held stage j-3 (drained)
+        swrite(j, R[(u + 2) % D]);
+        gload(min(j + D, nk - 1), R[(u + 2) % D]);
+        drain_lds_reads();                       // stage j visible before B_{kt+1}
+      }
+    }
+    return;
+  }
+  if (loader) {
+    // ======================= loader waves: the LDS-DMA ring =======================
+    uint32_t offA[TA::NI], offB[TB::NI];
+    TA::offsets(g.lda, wv, lane, offA);
+    TB::offsets(g.ldb, wv, lane, offB);
+    const bf16_t* pa = g.a + (long)m0 * g.lda;
+    const bf16_t* pb = g.b + (long)n0 * g.ldb;
+    auto issue = [&](int kt) {
+      char* sa = smem + (kt % NSTAGE) * G::STAGE;
+      TA::load_sv(pa + kt * BK, offA, sa, wv);
+      TB::load_sv(pb + kt * BK, offB, sa + G::A_BYTES, wv);
+    };
+#pragma unroll
+    for (int s = 0; s < NSTAGE; ++s)
+      if (s < nk) issue(s);
+    // B_init certifies stage 0: stages 1 .. min(nk, NSTAGE) - 1 may stay in flight
+    wait_stages<GLDS, NSTAGE - 1>(min(nk, NSTAGE) - 1);
+    nt_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      // B_kt certifies stage kt + 1; stages issued so far: 0 .. min(nk, kt + NSTAGE) - 1
+      if (kt + 1 < nk) wait_stages<GLDS, NSTAGE - 1>(min(nk, kt + NSTAGE) - 1 - (kt + 1));
+      nt_barrier();
+      if (DLTB_NT_ABL != 2 && kt + NSTAGE < nk) issue(kt + NSTAGE);  // into stage kt's slot: its reads were drained
+    }
+    return;
+  }
+
+  // ======================= consumer waves: LDS fragments -> MFMA =======================
+  f32x16 acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x16{};
+  NtFrags<BM, BN, BK> f0, f1;
+  nt_barrier();                  // B_init: stage 0 landed
+  f0.read(smem, wm, wn, r, h);
+  drain_lds_reads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    nt_barrier();                // B_kt: stage kt + 1 landed
+    f1.read(smem + ((kt + 1) % NSTAGE) * G::STAGE, wm, wn, r, h);
+    f0.mma(acc);
+    drain_lds_reads();                           // stage kt+1's reads done before B_{kt+1}
+    nt_barrier();                // B_{kt+1}: stage kt + 2 landed
+    f0.read(smem + ((kt + 2) % NSTAGE) * G::STAGE, wm, wn, r, h);   // (past the end: unused, no DMA in flight)
+    f1.mma(acc);
+    drain_lds_reads();
+  }
+
+  // ---- epilogue: lane -> row m, register group q -> columns n .. n+3
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+    const int m = m0 + wm * G::WM + 32 * i + r;
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = n0 + wn * G::WN + 32 * j + 8 * q + 4 * h;
+        float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        if (g.bias) {
+          const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
+          v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+        }
+        bf16_t* cp = g.c + (size_t)m * g.ldc + n;
+        if (g.accumulate) {
+          const uint2 old = *reinterpret_cast<const uint2*>(cp);
+          v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+        }
+        uint2 o;
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(cp) = o;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int NSTAGE, int RD = 0>
+void launch_nt(const NtArgs& g, hipStream_t st) {
+  constexpr int smem = NSTAGE * NtGeo<BM, BN, BK>::STAGE;
+  static_assert(smem <= 163840, "LDS budget");
+  static_assert(RD == 0 || NSTAGE == 3, "register-staged loaders write two stages ahead into a 3-slot ring");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NSTAGE, RD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NSTAGE, RD>), dim3(tiles), dim3(512), smem, st, g);
+}
+
+// tile configs: BM x BN, k-step BK, ring depth (what fits in 160 KB of LDS)
+struct NtCfg {
+  int bm, bn, bk;
+};
+constexpr NtCfg kNtCfgs[] = {{128, 64, 64}, {128, 128, 64}, {128, 192, 32}, {128, 256, 32},
+                             {256, 128, 32}, {64, 128, 64}, {128, 64, 64}};
+constexpr int kNtNumCfgs = sizeof(kNtCfgs) / sizeof(kNtCfgs[0]);
+
+void launch_cfg(int cfg, const NtArgs& g, hipStream_t st) {
+  switch (cfg) {
+    case 0: launch_nt<128, 64, 64, 6>(g, st); break;
+    case 1: launch_nt<128, 128, 64, 5>(g, st); break;
+    case 2: launch_nt<128, 192, 32, 8>(g, st); break;
+    case 3: launch_nt<128, 256, 32, 6>(g, st); break;
+    case 4: launch_nt<256, 128, 32, 6>(g, st); break;
+    case 5: launch_nt<64, 128, 64, 6>(g, st); break;
+    default: launch_nt<128, 64, 64, 3, 4>(g, st); break;     // register-staged loaders (A/B only)
+  }
+}
+
+}  // namespace
+
+static bool nt_fits(int c, int M, int N, int K) {
+  const NtCfg t = kNtCfgs[c];
+  const int unroll = c == 6 ? 4 : 2;                      // k-steps per unrolled loop body
+  return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % (unroll * t.bk) == 0;
+}
+
+int dltb_gemm_nt_pick(int M, int N, int K) {
+  // the config whose tile count is closest to one workgroup per CU (256); ties keep the earlier
+  // (BK = 64 before BK = 32 for the same tile)
+  int best = -1, bestd = 1 << 30;
+  for (int c = 0; c < kNtNumCfgs; ++c) {
+    if (!nt_fits(c, M, N, K)) continue;
+    const int tiles = (M / kNtCfgs[c].bm) * (N / kNtCfgs[c].bn);
+    const int d = tiles > 256 ? (tiles - 256) * 2 : 256 - tiles;
+    if (d < bestd) {
+      bestd = d;
+      best = c;
+    }
+  }
+  return best;
+}
+
+bool dltb_gemm_nt_supported(int M, int N, int K, int cfg) {
+  if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
+  return cfg >= 0 && cfg < kNtNumCfgs && nt_fits(cfg, M, N, K);
+}
+
+int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st) {
+  if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
+  if (!dltb_gemm_nt_supported(M, N, K, cfg)) return -1;
+  NtArgs g{};
+  g.a = (const bf16_t*)a;
+  g.b = (const bf16_t*)b;
+  g.c = (bf16_t*)c;
+  g.bias = (const bf16_t*)bias;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.gm = gm;
+  g.accumulate = accumulate;
+  launch_cfg(cfg, g, st);
+  return cfg;
+}

@@ -148,6 +148,12 @@ int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* pa
               long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
               const float* alpha, hipStream_t st, int stages = 0);
 
+// ---- gemm_nt.hip: C[M,N] = A[M][K] B[N][K]^T (+bias) (+C), bf16, one workgroup per CU tile grid
+int dltb_gemm_nt_pick(int M, int N, int K);
+bool dltb_gemm_nt_supported(int M, int N, int K, int cfg);
+int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st);
+
 // device-scalar helpers (head backward: no host sync)
 void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,
                     hipStream_t st);

@@ -29,6 +29,7 @@ DLTB_DEV f32x16 mfma32(bfx8 a, bfx8 b, f32x16 c) {
 
 template <int D>
 DLTB_DEV int swz(int row) {
+  if constexpr (D == 32) return (row >> 2) & 3;   // 64-byte rows: 4 rows per 256-byte bank row
   if constexpr (D == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
   else return ((row & 3) << 2) | ((row >> 2) & 3);
 }

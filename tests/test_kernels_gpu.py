@@ -264,6 +264,27 @@ def test_gemm(tn, M, N, K, cfg, splits, pf, gm, stages):
     close(acc, ref32 + prev.float(), 0.1, 2e-2, "gemm accumulate")
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, -1])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (512, 768, 256), (2048, 1024, 1024)])
+@pytest.mark.parametrize("gm", [1, 4])
+def test_gemm_nt(cfg, M, N, K, gm):
+    """Own NT GEMM (csrc/gemm_nt.hip: loader / consumer waves, LDS-DMA or register-staged ring) vs
+    fp32 torch: bias, accumulate, a row-strided A view, and the one-workgroup-per-CU default pick."""
+    C_ = ext()
+    if not C_.gemm_nt_supported(M, N, K, cfg):
+        pytest.skip("tile config does not divide this shape")
+    a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
+    a = a_full[:, 32:K + 32]
+    ref32 = a.float() @ b.float().t()
+    bias = rnd(N)
+    out = C_.gemm_nt(a, b, None, bias, False, cfg, gm)
+    close(out, ref32 + bias.float(), 0.05, 2e-2, "gemm_nt + bias")
+    prev = rnd(M, N)
+    acc = prev.clone()
+    C_.gemm_nt(a, b, acc, None, True, cfg, gm)
+    close(acc, ref32 + prev.float(), 0.05, 2e-2, "gemm_nt accumulate")
+
+
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
