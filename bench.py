@@ -84,6 +84,9 @@ def build_parser():
                     help="PREDICTION mode: one process on one GPU plays rank 0 of an N-rank job -- real N-rank "
                          "layouts, shards and buckets, every collective an alpha-beta-paced kernel on a "
                          "side stream (DLTB_COMM=emulate:N, comm/collectives.py); value = N x this rank's tok/s")
+    ap.add_argument("--no-calibrate", action="store_true",
+                    help="skip the in-job collective calibration at world > 1 (bucket size and comm model then "
+                         "come from profiles/xgmi_buckets.json or the defaults)")
     ap.add_argument("--host-check", action="store_true",
                     help="after the timed steps: host enqueue time per step while the GPU is held busy "
                          "(is the eager step host-bound?)")
@@ -161,6 +164,14 @@ def run_rank(args) -> int:
         with torch.device(device):          # random init straight into HBM
             model = build_model(mcfg)
         eworld = args.emulate or world     # the job's rank count (emulated or real)
+        fabric = None
+        from dltb.comm.topology import calibrate_fabric, measured_params
+        if (world > 1 and not args.no_calibrate and measured_params(world)[2] == "default"
+                and (not cuda or os.environ.get("DLTB_COMM", "rccl") != "host")):
+            # no measured sweep for this world size (profiles/xgmi_buckets.json): the alpha-beta of
+            # THIS job's fabric (RCCL over xGMI on the GPU node) before the buckets are planned;
+            # outside the timed region
+            fabric = calibrate_fabric(device, sizes_mb=(4, 16, 64) if cuda else (0.25, 1.0))
         bucket_mb = args.bucket_mb if args.bucket_mb is not None else recommend_bucket_mb(eworld)
         h = argparse.Namespace(strategy=args.strategy, deepspeed_config=args.deepspeed_config, fsdp_config=None,
                                grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype=args.dtype,
@@ -291,6 +302,9 @@ def run_rank(args) -> int:
                 "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
                 "gemm_tuning": tmode,
                 "hip_graphs": graphed,
+                "fabric_calibration": ({"fits": fabric["fits"], "rows": fabric["rows"],
+                                        "bucket_mb_from": "calibrated" if args.bucket_mb is None else "flag"}
+                                       if fabric else None),
             }
             if args.emulate:
                 out.update({

@@ -72,15 +72,76 @@ def fit_alpha_beta(rows, op: str, world: int):
     return max(alpha, 1.0), f / (slope * 1e3)
 
 
+# (world, op) -> (alpha_us, bus_GBps): fitted by calibrate_fabric() in THIS job, on its own ranks
+_CALIBRATED = {}
+
+
 def measured_params(world: int, op: str = "reduce_scatter", path: str = None):
-    """(alpha_us, bus_GBps, source) for ``world`` ranks: the fit of the measured sweep when the
-    profile holds this world size, else the conservative defaults."""
+    """(alpha_us, bus_GBps, source) for ``world`` ranks: this job's own calibration
+    (:func:`calibrate_fabric`, source "calibrated"), else the fit of the suite's measured sweep when
+    the profile holds this world size ("measured"), else the conservative defaults ("default")."""
+    cal = _CALIBRATED.get((world, op))
+    if cal is not None:
+        return cal[0], cal[1], "calibrated"
     prof = load_profile(path)
     rows = (prof or {}).get("worlds", {}).get(str(world)) if prof else None
     fit = fit_alpha_beta(rows, op, world) if rows else None
     if fit is not None:
         return fit[0], fit[1], "measured"
     return DEFAULT_ALPHA_US, DEFAULT_BUS_GBPS, "default"
+
+
+def calibrate_fabric(device, sizes_mb=(4, 16, 64), iters: int = 5, dtype=None, group=None,
+                     ops=("reduce_scatter", "all_reduce", "all_gather")) -> dict:
+    """Time this job's own collectives before the engine builds its buckets: each op at each size,
+    ``iters`` calls between a barrier + device sync (the MAX over ranks), then the alpha-beta fit of
+    :func:`fit_alpha_beta` per op.  The fits replace the defaults / suite profile for this process
+    (``measured_params`` source "calibrated"), so ``recommend_bucket_mb`` and the comm model use the
+    fabric the job actually runs on -- the 8 x MI355X xGMI mesh at the driver's scaling runs, where
+    no profile from a multi-GPU box exists yet.  Collective calls only (no process-group setup);
+    ~0.1-0.3 s at 8 ranks.  Returns {"world", "rows": [...], "fits": {op: {"alpha_us", "bus_GBps"}}}
+    (rows in the profile format of scripts/bench_collectives.py)."""
+    import time
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    cuda = device.type == "cuda"
+    dtype = dtype or (torch.bfloat16 if cuda else torch.float32)
+    esz = torch.empty((), dtype=dtype).element_size()
+    sync = (lambda: torch.cuda.synchronize(device)) if cuda else (lambda: None)
+    rows = []
+    for op in ops:
+        for mb in sizes_mb:
+            n = max(world, (int(mb * (1 << 20)) // esz) // world * world)
+            full = torch.ones(n, dtype=dtype, device=device)
+            part = torch.ones(n // world, dtype=dtype, device=device)
+            if op == "reduce_scatter":
+                call = lambda: dist.reduce_scatter_tensor(part, full, group=group)        # noqa: E731
+            elif op == "all_gather":
+                call = lambda: dist.all_gather_into_tensor(full, part, group=group)        # noqa: E731
+            else:
+                call = lambda: dist.all_reduce(full, group=group)                          # noqa: E731
+            for _ in range(2):
+                call()
+            sync()
+            dist.barrier(group=group)
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                call()
+            sync()
+            dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                              device=device if dist.get_backend(group) == "nccl" else "cpu")
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=group)
+            rows.append({"op": op, "bytes": n * esz, "time_us": float(dt.item()) / iters * 1e6,
+                         "dtype": str(dtype).replace("torch.", "")})
+            del full, part
+    fits = {}
+    for op in ops:
+        fit = fit_alpha_beta(rows, op, world)
+        if fit is not None:
+            fits[op] = {"alpha_us": fit[0], "bus_GBps": fit[1]}
+            _CALIBRATED[(world, op)] = fit
+    return {"world": world, "rows": rows, "fits": fits}
 
 
 def recommend_bucket_mb(world: int, overhead: float = 0.2, bus_gbps: float = None,

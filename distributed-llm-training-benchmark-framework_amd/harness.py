@@ -130,9 +130,7 @@ def _engine_for(args, model, device):
 def train(args):
     world, rank, local_rank = resolve_ranks(args.world_size, args.rank, args.local_rank)
     args.world_size, args.rank, args.local_rank = world, rank, local_rank
-    if args.bucket_mb is None:
-        from .comm.topology import recommend_bucket_mb
-        args.bucket_mb = recommend_bucket_mb(world)
+    auto_bucket = args.bucket_mb is None
     label = args.strategy_label or args.strategy
     if args.dtype == "auto":
         args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
@@ -143,6 +141,14 @@ def train(args):
     device = setup_distributed(world, rank, local_rank, args.master_addr, args.master_port, args.device,
                                args.timeout_min, args.debug_collectives)
     is_main = rank == 0
+    fabric = None
+    if auto_bucket:
+        from .comm.topology import calibrate_fabric, measured_params, recommend_bucket_mb
+        if (world > 1 and measured_params(world)[2] == "default"
+                and (device.type != "cuda" or os.environ.get("DLTB_COMM", "rccl") != "host")):
+            # this job's own collective alpha-beta before the engine plans its buckets (bench.py does the same)
+            fabric = calibrate_fabric(device, sizes_mb=(4, 16, 64) if device.type == "cuda" else (0.25, 1.0))
+        args.bucket_mb = recommend_bucket_mb(world)
     try:
         if device.type == "cuda" and not ext_available():
             raise RuntimeError("dltb._C is not built: run `python csrc/build.py` (the GPU path has no fallback)")
@@ -302,6 +308,7 @@ def train(args):
                                                                         and not runner.disabled) else None),
             "comm_ops_timed": {k: dict(v) for k, v in engine.comm.stats.items()},
             "comm_topology": comm_describe(world) if (is_main and device.type == "cuda") else None,
+            "fabric_calibration": fabric,
             "memory": engine.memory_report(),
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
             "accum_semantics": args.accum_semantics, "grad_reduce": args.grad_reduce, "dtype": args.dtype,

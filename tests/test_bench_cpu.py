@@ -42,6 +42,11 @@ def test_bench_self_launch_two_ranks():
     assert rec["wire_bytes_per_step"] > 0
     assert abs(rec["wire_bytes_per_step"] - rec["wire_bytes_per_step_model"]) / rec["wire_bytes_per_step_model"] < 0.01
     assert rec["comm_wait_ms"] is not None and rec["mean_loss"] > 0
+    # the job calibrated its own collectives before planning buckets (gloo here, RCCL on GPUs)
+    cal = rec["fabric_calibration"]
+    assert {r["op"] for r in cal["rows"]} == {"reduce_scatter", "all_reduce", "all_gather"}
+    assert all(r["time_us"] > 0 and r["bytes"] > 0 for r in cal["rows"])
+    assert cal["bucket_mb_from"] == "calibrated" and rec["config"]["bucket_mb"] >= 1
 
 
 def test_bench_window_is_labelled_zero1():
