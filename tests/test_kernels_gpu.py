@@ -85,6 +85,8 @@ def test_gelu_and_bias_grad():
     f = rnd(N, k)
     C = ext()
     close(C.gelu_fwd(f), ref.gelu_fwd(f), 1e-2, 1e-2, "gelu")
+    f_odd = rnd(7, 24)                           # 21 chunks of 8: the two-chunk pass's tail
+    close(C.gelu_fwd(f_odd), ref.gelu_fwd(f_odd), 1e-2, 1e-2, "gelu odd")
     dg = rnd(N, k)
     db = torch.zeros(k, device=DEV, dtype=torch.bfloat16)
     rdb = db.clone()
