@@ -22,6 +22,13 @@ MI355X-native design on ``torch.distributed`` (RCCL over xGMI):
   ZeRO-2, so they never cost a fetch.
 * Optimizer: one fused AdamW launch over the rank's owner space [persistent chunk | group shards];
   the bf16 shard is written in place and becomes the next all-gather's input.
+* Precision of the reduction: gradients are reduce-scattered in the compute dtype.  In the fp16
+  (reference-precision FSDP) runs that is the loss-scaled fp16 gradient, where the reference's
+  torch FSDP (no mixed precision) reduces fp32: a sum over N ranks reaches fp16's range about N
+  times sooner, so the dynamic loss scaler may back off more often at 8 ranks than the reference
+  would.  Parity unpinned; bench.py and the harness report the scaler's skipped-step count
+  (``loss_scaler.optimizer_steps_skipped``) so a run shows whether it happened.  DDP has the fp32
+  communication option (``grad_comm_dtype``, replicated.py).
 """
 import os
 

@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# PMC counters of the attention kernels (TinyGPT-A shape), one rocprofv3 pass per counter group.
+# PMC counters of the attention kernels (TinyGPT-A shape; SHAPES=m7b for the Mistral shape), one rocprofv3
+# pass per counter group.
 #   ./scripts/pmc_attn.sh OUTDIR
 set -uo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
@@ -10,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 pass() {
   local name="$1"; shift
   timeout -s KILL 90 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/$name" -o run -- \
-    python3 "$ROOT/scripts/bench_attn.py" --iters 5 --shapes tinygpt_a > "$OUT/$name.log" 2>&1
+    python3 "$ROOT/scripts/bench_attn.py" --iters 5 --shapes "${SHAPES:-tinygpt_a}" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "pass $name rc=$rc"
   return $rc
