@@ -540,11 +540,22 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   const int T = P.T, nT = T / kTile;
   int kb, bk;
   const int gsplit = P.gsplit;
-  block_coords(T / kBlockRows, P.B * P.Hkv * gsplit, false, kb, bk);
+  if (CAUSAL && gsplit > 1) {
+    // head-split causal grids: key block (the work: query tiles kb*2 .. nT-1) is the SLOW index, so
+    // the grid is dispatched heaviest first over all heads and the workgroups that free their slot
+    // early pick up the light blocks (greedy longest-first balance).  The (head, split) index is
+    // fast: with nbk % 8 == 0 the workgroups of one XCD (b, b+8, ...) cover nbk/8 of them and share
+    // their Q / dO tiles in its L2.  (block_coords' XCD remap cycled kb 0..nkb-1 once per 8 x nkb
+    // workgroups, so heavy blocks kept arriving until the end of the grid.)
+    const int nbk = P.B * P.Hkv * gsplit;
+    kb = blockIdx.x / nbk;
+    bk = blockIdx.x - kb * nbk;
+  } else {
+    block_coords(T / kBlockRows, P.B * P.Hkv * gsplit, false, kb, bk);
+  }
   const int gs = bk % gsplit;
   bk /= gsplit;
-  // one workgroup per key block: all resident at once, heaviest (first keys) last.  Head-split
-  // grids (causal GQA) are several waves deep, so they go heaviest first (greedy balance)
+  // one workgroup per key block and KV head: all resident at once, heaviest (first keys) last
   if (CAUSAL && gsplit == 1) kb = T / kBlockRows - 1 - kb;
   const int b = bk / P.Hkv, hk = bk % P.Hkv;
   const int G = P.Hq / P.Hkv / gsplit, g0 = gs * G;   // this workgroup's query heads of the group
