@@ -547,6 +547,8 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
     // fast: with nbk % 8 == 0 the workgroups of one XCD (b, b+8, ...) cover nbk/8 of them and share
     // their Q / dO tiles in its L2.  (block_coords' XCD remap cycled kb 0..nkb-1 once per 8 x nkb
     // workgroups, so heavy blocks kept arriving until the end of the grid.)
+    // (pairing key blocks kb and nkb-1-kb across the two halves of the grid measured 18 % slower:
+    // profiles/dkdv_lpt_map_m7b_r3.txt)
     const int nbk = P.B * P.Hkv * gsplit;
     kb = blockIdx.x / nbk;
     bk = blockIdx.x - kb * nbk;
