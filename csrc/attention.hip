@@ -46,6 +46,9 @@
 #define DLTB_ATTN_PIPE 0
 #endif
 
+#ifndef DLTB_ATTN_LPT
+#define DLTB_ATTN_LPT 1   // causal fwd / dQ grids heaviest-first (profiles/attn_lpt_order_m7b_r3.txt)
+#endif
 // key splits per workgroup at D = 64 (A/B builds: csrc/build.py --tag T -D DLTB_FWD_KS64=2)
 #ifndef DLTB_FWD_KS64
 #define DLTB_FWD_KS64 3
@@ -248,6 +251,17 @@ DLTB_DEV f32x16 splat16(float v) {
 // (last) query blocks first.
 DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
   const int L = blockIdx.x, total = nqb * nbh;
+#if DLTB_ATTN_LPT
+  if (causal && (nbh & 7) == 0) {
+    // causal grids several rounds deep: heaviest query blocks first over the WHOLE grid (greedy
+    // longest-first balance), each XCD (workgroups b, b+8, ...) on nbh/8 consecutive heads (one KV
+    // group's K / V in its L2 under GQA)
+    const int hpx = nbh >> 3, r = L >> 3;
+    bh = (L & 7) * hpx + r % hpx;
+    qb = nqb - 1 - r / hpx;
+    return;
+  }
+#endif
   int idx = L;
   if ((total & 7) == 0) idx = (L & 7) * (total >> 3) + (L >> 3);
   bh = idx / nqb;
