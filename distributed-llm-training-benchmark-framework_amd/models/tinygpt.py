@@ -360,6 +360,7 @@ class TinyGPT(nn.Module):
         key = (L, N, R, d, like.dtype, like.device)
         if self._lbuf_key != key:
             self._lbufs = None                       # free the old set before allocating the new one
+            self.__dict__.pop("_lbuf_views", None)   # (their cached views too)
             mk = lambda k: torch.empty(L, R * N, k, dtype=like.dtype, device=like.device)  # noqa: E731
             self._lbufs = SimpleNamespace(h1=mk(d), o=mk(d), h2=mk(d), g=mk(F), dqkv=mk(3 * d), dx1=mk(d),
                                           df=mk(F), dm=mk(d))
@@ -376,9 +377,18 @@ class TinyGPT(nn.Module):
             return None
         r = self.cfg.n_layer - 1 - i if getattr(self.rt, "wgrad_rows_reversed", True) else i
         pos, R, N = self._lbuf_win
-        out = SimpleNamespace(**{k: v[r, pos * N:(pos + 1) * N] for k, v in vars(b).items()})
-        out.window = R > 1
-        out.full = SimpleNamespace(**{k: v[r] for k, v in vars(b).items()}) if (R > 1 and pos == R - 1) else None
+        # the views of one (row, window position) never change while the buffers live: build them once
+        # (eight slices per block per micro-step were host time of every eager step)
+        ck = (r, pos, R, N, id(b))
+        cache = self.__dict__.setdefault("_lbuf_views", {})
+        out = cache.get(ck)
+        if out is None:
+            if len(cache) > 4 * self.cfg.n_layer * max(R, 1):
+                cache.clear()
+            out = SimpleNamespace(**{k: v[r, pos * N:(pos + 1) * N] for k, v in vars(b).items()})
+            out.window = R > 1
+            out.full = SimpleNamespace(**{k: v[r] for k, v in vars(b).items()}) if (R > 1 and pos == R - 1) else None
+            cache[ck] = out
         return out
 
     def forward(self, idx, targets=None, return_logits=False):
