@@ -123,3 +123,47 @@ def test_alpha_beta_fit_and_measured_bucket(tmp_path, monkeypatch):
     assert recommend_bucket_mb(8) == 64.0
     monkeypatch.setenv("DLTB_XGMI_PROFILE", str(tmp_path / "missing.json"))
     assert measured_params(8)[2] == "default"
+
+
+def _calib_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dltb.comm import topology as tp
+        res = tp.calibrate_fabric(torch.device("cpu"), sizes_mb=(0.25, 1.0), iters=2)
+        if rank == 0:
+            torch.save({"rows": res["rows"], "fits": res["fits"],
+                        "src": tp.measured_params(world)[2],
+                        "bucket": tp.recommend_bucket_mb(world)}, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_calibrate_fabric_world2(monkeypatch):
+    """In-job calibration on the job's own process group: one row per (op, size), every time
+    positive (the max over ranks), and a physical fit -- when it exists -- becomes the process's
+    'calibrated' alpha-beta, ahead of a suite profile."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "calib.pt")
+        mp.spawn(_calib_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        r = torch.load(out, weights_only=True)
+    assert len(r["rows"]) == 6 and {x["op"] for x in r["rows"]} == {"reduce_scatter", "all_reduce", "all_gather"}
+    assert all(x["time_us"] > 0 and x["bytes"] > 0 for x in r["rows"])
+    if "reduce_scatter" in r["fits"]:
+        assert r["src"] == "calibrated" and r["fits"]["reduce_scatter"]["bus_GBps"] > 0
+    assert r["bucket"] >= 1
+
+
+def test_calibrated_params_take_precedence(tmp_path, monkeypatch):
+    import json
+    from dltb.comm import topology as tp
+    p = tmp_path / "prof.json"
+    p.write_text(json.dumps({"worlds": {"8": [{"op": "reduce_scatter", "bytes": b, "time_us": 40 + b / 2.5e5}
+                                               for b in (1 << 20, 16 << 20)]}}))
+    monkeypatch.setenv("DLTB_XGMI_PROFILE", str(p))
+    assert tp.measured_params(8)[2] == "measured"
+    monkeypatch.setitem(tp._CALIBRATED, (8, "reduce_scatter"), (12.0, 400.0))
+    assert tp.measured_params(8) == (12.0, 400.0, "calibrated")
+    # 12 us at 400 GB/s: need 12/0.2 us * 400 GB/s / (7/8) = 27 MB -> 32 MiB
+    assert tp.recommend_bucket_mb(8) == 32.0
