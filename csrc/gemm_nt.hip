@@ -24,6 +24,10 @@
 // 0.8-0.9x on N = 3072 / 4096 (profiles/gemm_nt_r3.txt), so the step keeps hipBLASLt; this kernel
 // is the measured own-MFMA alternative (scripts/bench_gemm_nt.py) and its ablation builds
 // (DLTB_NT_ABL, scripts/probes/gemm_nt_abl.cpp) locate the bound.
+// Split-K (cfgs 7-9, fp32 planes): 128 x 128 x 2 splits runs the K-long N = 1024 products 1.03-1.15x
+// faster than hipBLASLt (fc2 22.3 vs 25.7 us, fc1 dgrad 22.2 vs 25.5, qkv dgrad 19.4 vs 19.9;
+// profiles/gemm_nt_splitk_r3.txt), but the consuming LayerNorm would then read 16 MB of fp32 planes
+// instead of 4 MB of bf16 (~2 us more per product), which leaves ~1% of a step: not wired in.
 #include "common.h"
 #include "launchers.h"
 #include "mfma_tiles.h"
@@ -43,6 +47,7 @@ struct NtArgs {
   int M, N, K;
   int gm;            // m-blocks per group of the tile walk
   int accumulate;
+  float* part;       // split-K configs: fp32 partial planes part[split][M][N] (bias folded into split 0)
 };
 
 template <int GLDS, int N>
@@ -76,7 +81,7 @@ struct NtGeo {
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
 };
 
-template <int BM, int BN, int BK>
+template <int BM, int BN, int BK, bool SWAP = false>
 struct NtFrags {
   using G = NtGeo<BM, BN, BK>;
   bfx8 a[G::KS][G::FM], b[G::KS][G::FN];
@@ -107,7 +112,10 @@ struct NtFrags {
 #pragma unroll
       for (int i = 0; i < G::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < G::FN; ++j) acc[i][j] = mfma32(b[s][j], a[s][i], acc[i][j]);   // lane <-> m
+        for (int j = 0; j < G::FN; ++j) {
+          if constexpr (SWAP) acc[i][j] = mfma32(a[s][i], b[s][j], acc[i][j]);    // lane <-> n
+          else acc[i][j] = mfma32(b[s][j], a[s][i], acc[i][j]);                   // lane <-> m
+        }
   }
 };
 
@@ -134,7 +142,15 @@ DLTB_DEV void nt_barrier() {
 // two k-steps before the consumers read it; the ring then needs only NSTAGE = 3 slots.  Plain vector
 // loads stream 120-128 GB/s per CU from L2 against 80-105 for LDS-DMA
 // (scripts/probes/l2_stream_probe.hip).
-template <int BM, int BN, int BK, int NSTAGE, int RD>
+//
+// SK > 1: split-K.  The grid is SK x tiles; split s multiplies the K range [s K/SK, (s+1) K/SK) and
+// stores its fp32 tile into plane s of g.part.  The MFMA operands are swapped (lane <-> n) so that
+// each store instruction writes two full 128-byte rows; the consumer of the planes (a LayerNorm that
+// reads the product as its input / its upstream gradient) sums them on its way in.  This halves the
+// per-CU operand stream of the K-long products (fc2, and the fc1 / qkv data gradients), whose tile
+// grids at M = 2048, N = 1024 would otherwise hold only 128 workgroups of 128 x 128 or stream
+// 1.57 MB per CU as 256 tiles of 128 x 64.
+template <int BM, int BN, int BK, int NSTAGE, int RD, int SK = 1>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
   using G = NtGeo<BM, BN, BK>;
   using TA = GldsTile<BK, BM, true>;
@@ -150,9 +166,11 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
 
   // ---- tile walk: XCD-major, then groups of gm m-blocks x all n-blocks
   const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
-  const int L = blockIdx.x;
+  const int L = blockIdx.x, blocks = tiles * SK;
   int idx = L;
-  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  if ((blocks & 7) == 0) idx = (L & 7) * (blocks >> 3) + (L >> 3);
+  const int split = SK > 1 ? idx / tiles : 0;    // split-major: each XCD holds a contiguous tile range of one split
+  if (SK > 1) idx -= split * tiles;
   int mb, nb;
   if (g.gm > 1 && tiles_m % g.gm == 0) {
     const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
@@ -163,8 +181,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
     nb = idx - mb * tiles_n;
   }
   const int m0 = mb * BM, n0 = nb * BN;
-  const int nk = g.K / BK;                       // even (host check)
-  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * BK == g.K && nk >= 2 && (nk & 1) == 0);
+  const int nk = g.K / (BK * SK);                // k-steps of this split: even (host check)
+  const long k0 = (long)split * nk * BK;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * BK * SK == g.K && nk >= 2 && (nk & 1) == 0);
 
   if (RD > 0 && loader) {
     // ======================= loader waves: register-staged ring =======================
@@ -172,8 +191,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
     uint32_t offA[NA], offB[NB];
     TA::offsets(g.lda, wv, lane, offA);
     TB::offsets(g.ldb, wv, lane, offB);
-    const char* pa = (const char*)(g.a + (long)m0 * g.lda);
-    const char* pb = (const char*)(g.b + (long)n0 * g.ldb);
+    const char* pa = (const char*)(g.a + (long)m0 * g.lda + k0);
+    const char* pb = (const char*)(g.b + (long)n0 * g.ldb + k0);
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     u32x4 R[D][NI];
     auto gload = [&](int stage, u32x4 (&r)[NI]) {
@@ -221,8 +240,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
     uint32_t offA[TA::NI], offB[TB::NI];
     TA::offsets(g.lda, wv, lane, offA);
     TB::offsets(g.ldb, wv, lane, offB);
-    const bf16_t* pa = g.a + (long)m0 * g.lda;
-    const bf16_t* pb = g.b + (long)n0 * g.ldb;
+    const bf16_t* pa = g.a + (long)m0 * g.lda + k0;
+    const bf16_t* pb = g.b + (long)n0 * g.ldb + k0;
     auto issue = [&](int kt) {
       char* sa = smem + (kt % NSTAGE) * G::STAGE;
       TA::load_sv(pa + kt * BK, offA, sa, wv);
@@ -249,7 +268,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
   for (int i = 0; i < G::FM; ++i)
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x16{};
-  NtFrags<BM, BN, BK> f0, f1;
+  NtFrags<BM, BN, BK, (SK > 1)> f0, f1;
   nt_barrier();                  // B_init: stage 0 landed
   f0.read(smem, wm, wn, r, h);
   drain_lds_reads();
@@ -264,6 +283,22 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
     drain_lds_reads();
   }
 
+  if constexpr (SK > 1) {
+    // ---- split-K epilogue: lane -> column n, register e -> row (e & 3) + 8 (e >> 2) + 4 h (fp32 planes)
+    float* pp = g.part + (size_t)split * g.M * g.N;
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+      const int n = n0 + wn * G::WN + 32 * j + r;
+      const float bv = (g.bias && split == 0) ? bf2f(g.bias[n]) : 0.f;
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i) {
+        const int mb0 = m0 + wm * G::WM + 32 * i + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pp[(size_t)(mb0 + (e & 3) + 8 * (e >> 2)) * g.N + n] = acc[i][j][e] + bv;
+      }
+    }
+    return;
+  }
   // ---- epilogue: lane -> row m, register group q -> columns n .. n+3
 #pragma unroll
   for (int i = 0; i < G::FM; ++i) {
@@ -292,27 +327,28 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
   }
 }
 
-template <int BM, int BN, int BK, int NSTAGE, int RD = 0>
+template <int BM, int BN, int BK, int NSTAGE, int RD = 0, int SK = 1>
 void launch_nt(const NtArgs& g, hipStream_t st) {
   constexpr int smem = NSTAGE * NtGeo<BM, BN, BK>::STAGE;
   static_assert(smem <= 163840, "LDS budget");
   static_assert(RD == 0 || NSTAGE == 3, "register-staged loaders write two stages ahead into a 3-slot ring");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NSTAGE, RD>,
+    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NSTAGE, RD, SK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int tiles = (g.M / BM) * (g.N / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NSTAGE, RD>), dim3(tiles), dim3(512), smem, st, g);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NSTAGE, RD, SK>), dim3(tiles * SK), dim3(512), smem, st, g);
 }
 
 // tile configs: BM x BN, k-step BK, ring depth (what fits in 160 KB of LDS)
 struct NtCfg {
-  int bm, bn, bk;
+  int bm, bn, bk, sk;
 };
-constexpr NtCfg kNtCfgs[] = {{128, 64, 64}, {128, 128, 64}, {128, 192, 32}, {128, 256, 32},
-                             {256, 128, 32}, {64, 128, 64}, {128, 64, 64}};
+constexpr NtCfg kNtCfgs[] = {{128, 64, 64, 1},  {128, 128, 64, 1}, {128, 192, 32, 1}, {128, 256, 32, 1},
+                             {256, 128, 32, 1}, {64, 128, 64, 1},  {128, 64, 64, 1},  {128, 128, 64, 2},
+                             {128, 64, 64, 2},  {256, 128, 32, 2}};
 constexpr int kNtNumCfgs = sizeof(kNtCfgs) / sizeof(kNtCfgs[0]);
 
 void launch_cfg(int cfg, const NtArgs& g, hipStream_t st) {
@@ -323,7 +359,10 @@ void launch_cfg(int cfg, const NtArgs& g, hipStream_t st) {
     case 3: launch_nt<128, 256, 32, 6>(g, st); break;
     case 4: launch_nt<256, 128, 32, 6>(g, st); break;
     case 5: launch_nt<64, 128, 64, 6>(g, st); break;
-    default: launch_nt<128, 64, 64, 3, 4>(g, st); break;     // register-staged loaders (A/B only)
+    case 6: launch_nt<128, 64, 64, 3, 4>(g, st); break;      // register-staged loaders (A/B only)
+    case 7: launch_nt<128, 128, 64, 5, 0, 2>(g, st); break;  // split-K 2 -> fp32 planes
+    case 8: launch_nt<128, 64, 64, 6, 0, 2>(g, st); break;
+    default: launch_nt<256, 128, 32, 6, 0, 2>(g, st); break;
   }
 }
 
@@ -332,7 +371,7 @@ void launch_cfg(int cfg, const NtArgs& g, hipStream_t st) {
 static bool nt_fits(int c, int M, int N, int K) {
   const NtCfg t = kNtCfgs[c];
   const int unroll = c == 6 ? 4 : 2;                      // k-steps per unrolled loop body
-  return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % (unroll * t.bk) == 0;
+  return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % (unroll * t.bk * t.sk) == 0;
 }
 
 int dltb_gemm_nt_pick(int M, int N, int K) {
@@ -340,7 +379,7 @@ int dltb_gemm_nt_pick(int M, int N, int K) {
   // (BK = 64 before BK = 32 for the same tile)
   int best = -1, bestd = 1 << 30;
   for (int c = 0; c < kNtNumCfgs; ++c) {
-    if (!nt_fits(c, M, N, K)) continue;
+    if (kNtCfgs[c].sk > 1 || !nt_fits(c, M, N, K)) continue;   // split-K only on request
     const int tiles = (M / kNtCfgs[c].bm) * (N / kNtCfgs[c].bn);
     const int d = tiles > 256 ? (tiles - 256) * 2 : 256 - tiles;
     if (d < bestd) {
@@ -351,15 +390,18 @@ int dltb_gemm_nt_pick(int M, int N, int K) {
   return best;
 }
 
+int dltb_gemm_nt_splits(int cfg) { return cfg >= 0 && cfg < kNtNumCfgs ? kNtCfgs[cfg].sk : 1; }
+
 bool dltb_gemm_nt_supported(int M, int N, int K, int cfg) {
   if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
   return cfg >= 0 && cfg < kNtNumCfgs && nt_fits(cfg, M, N, K);
 }
 
 int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st) {
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part) {
   if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
   if (!dltb_gemm_nt_supported(M, N, K, cfg)) return -1;
+  if (kNtCfgs[cfg].sk > 1 && (part == nullptr || accumulate)) return -1;
   NtArgs g{};
   g.a = (const bf16_t*)a;
   g.b = (const bf16_t*)b;
@@ -373,6 +415,7 @@ int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long l
   g.K = K;
   g.gm = gm;
   g.accumulate = accumulate;
+  g.part = part;
   launch_cfg(cfg, g, st);
   return cfg;
 }

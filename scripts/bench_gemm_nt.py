@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The own NT GEMM (csrc/gemm_nt.hip) against hipBLASLt on the per-layer products of a step.
 
-    python scripts/bench_gemm_nt.py [--model A|M7B] [--iters 50] [--sweep]
+    python scripts/bench_gemm_nt.py [--model A|M7B] [--iters 50] [--sweep] [--split]
 
 Every product is C[M, N] = A[M, K] B[N, K]^T (+ bias): the forward x W^T and the data gradient
 dY (W^T)^T against the engine's cached W^T.  Prints hipBLASLt (the tuned table entry when the
@@ -21,7 +21,8 @@ from dltb.ops import blaslt  # noqa: E402
 from dltb.ops._ext import ext  # noqa: E402
 
 CFGS = {0: "128x64k64", 1: "128x128k64", 2: "128x192k32", 3: "128x256k32", 4: "256x128k32", 5: "64x128k64",
-        6: "128x64r4"}
+        6: "128x64r4", 7: "128x128s2", 8: "128x64s2", 9: "256x128s2"}
+SPLIT = (7, 8, 9)   # split-K configs: fp32 planes [2, M, N], summed by the consumer
 
 
 def products(model):
@@ -67,6 +68,7 @@ def main():
     ap.add_argument("--model", default="A")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--split", action="store_true", help="also time the split-K configs (fp32 planes)")
     a = ap.parse_args()
     C = ext()
     blaslt.load()
@@ -92,7 +94,13 @@ def main():
         if a.sweep:
             variants += [(f"c{c}g{gm}", c, gm) for c in CFGS for gm in (1, 4)
                          if C.gemm_nt_supported(M, N, K, c)]
-        fns = [lib] + [(lambda c=c, gm=gm: C.gemm_nt(x, w, y_own, bias, False, c, gm)) for _, c, gm in variants]
+        if a.split:
+            variants += [(f"c{c}g{gm}", c, gm) for c in SPLIT for gm in (1, 4) if C.gemm_nt_supported(M, N, K, c)]
+        planes = torch.empty(2, M, N, device="cuda", dtype=torch.float32)
+
+        def own(c, gm):
+            return C.gemm_nt(x, w, planes if c in SPLIT else y_own, bias, False, c, gm)
+        fns = [lib] + [(lambda c=c, gm=gm: own(c, gm)) for _, c, gm in variants]
         ts = graph_time(fns, a.iters)
         lib()
         err_ref = (y_ref.float() - ref).abs().max().item()
@@ -100,9 +108,9 @@ def main():
         print(f"{name:11s} M{M} N{N:6d} K{K:6d}  hipBLASLt {ts[0]:7.1f} us {fl / ts[0] / 1e6:6.0f} TF/s "
               f"(err {err_ref:.3g})", flush=True)
         for (tag, c, gm), t in zip(variants, ts[1:]):
-            C.gemm_nt(x, w, y_own, bias, False, c, gm)
+            out = own(c, gm)
             torch.cuda.synchronize()
-            err = (y_own.float() - ref).abs().max().item()
+            err = ((out.sum(0) if c in SPLIT else out.float()) - ref).abs().max().item()
             pick = CFGS.get(c, "pick")
             print(f"    {tag:6s} {pick:11s} {t:7.1f} us {fl / t / 1e6:6.0f} TF/s  x{ts[0] / t:4.2f}  err {err:.3g}"
                   + ("  MISMATCH" if err > 2 * err_ref + 0.05 else ""), flush=True)

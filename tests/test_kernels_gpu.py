@@ -287,6 +287,24 @@ def test_gemm_nt(cfg, M, N, K, gm):
     close(acc, ref32 + prev.float(), 0.05, 2e-2, "gemm_nt accumulate")
 
 
+@pytest.mark.parametrize("cfg", [7, 8, 9])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (2048, 1024, 4096), (512, 384, 1536)])
+def test_gemm_nt_splitk(cfg, M, N, K):
+    """Split-K NT GEMM: two fp32 planes (bias in plane 0) whose sum is the fp32 product."""
+    C_ = ext()
+    if not C_.gemm_nt_supported(M, N, K, cfg):
+        pytest.skip("tile config does not divide this shape")
+    a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
+    a = a_full[:, 32:K + 32]
+    bias = rnd(N)
+    ref32 = a.float() @ b.float().t()
+    planes = C_.gemm_nt(a, b, None, bias, False, cfg, 4)
+    assert planes.dtype == torch.float32 and tuple(planes.shape) == (2, M, N)
+    close(planes.sum(0), ref32 + bias.float(), 2e-3, 1e-3, "gemm_nt split-K planes")
+    ref_lo = a[:, :K // 2].float() @ b[:, :K // 2].float().t()
+    close(planes[0], ref_lo + bias.float(), 2e-3, 1e-3, "gemm_nt split-K plane 0 = first half of K + bias")
+
+
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
