@@ -10,7 +10,7 @@
 // 80-105 GB/s by LDS-DMA and 112-128 GB/s by plain vector loads, so these products are bound by
 // that per-CU operand stream (a 128 x 64 tile at K = 4096 is 1.57 MB per CU), not by the MFMAs.
 //
-// Structure (512 threads, one workgroup per CU, one tile per workgroup, no split-K):
+// Structure (512 threads, one workgroup per CU, one tile per workgroup; split-K configs below):
 //   * waves 4-7 (loaders) fill an NSTAGE-deep LDS ring by LDS-DMA (global_load_lds_dwordx4,
 //     swizzle on the source address, mfma_tiles.h; per-lane offsets computed once, wave-uniform
 //     base advanced by SALU) -- or, with RD > 0, stage RD k-steps in VGPRs and ds_write them;
