@@ -124,6 +124,10 @@ def resolve_precision(args):
     """--dtype / --grad-comm-dtype auto -> the reference's precision per strategy (harness.py)."""
     if args.dtype == "auto":
         args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
+        if args.strategy in ("zero2", "zero3") and args.deepspeed_config:   # the config's precision
+            from dltb.parallel.ds_config import ds_precision
+            from dltb.parallel.strategy import load_deepspeed_config
+            args.dtype = ds_precision(load_deepspeed_config(args.deepspeed_config))
     if args.grad_comm_dtype == "auto":
         args.grad_comm_dtype = "fp32" if (args.strategy == "ddp" and args.dtype == "fp16") else "compute"
     return args
@@ -273,6 +277,7 @@ def run_rank(args) -> int:
                            "global_batch": args.per_device_batch * accum * world,
                            "micro_batch_per_gpu": args.per_device_batch,
                            "grad_accum": accum,
+                           "grad_accum_cli": args.grad_accum,
                            "seq_len": args.seq_len,
                            "parallelism": f"{label}-dp{world}",
                            "grad_reduce": ecfg.extra.get("grad_reduce"),
@@ -302,6 +307,7 @@ def run_rank(args) -> int:
                 "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
                 "gemm_tuning": tmode,
                 "hip_graphs": graphed,
+                "ds_config_keys_ignored": sorted((ecfg.extra.get("ds_keys") or {}).get("ignored", {})),
                 "fabric_calibration": ({"fits": fabric["fits"], "rows": fabric["rows"],
                                         "bucket_mb_from": "calibrated" if args.bucket_mb is None else "flag"}
                                        if fabric else None),

@@ -356,6 +356,12 @@ class Comm:
         w = dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
         return self._track(w, async_op) if track else (w if async_op else _DONE)
 
+    def global_rank(self, r: int) -> int:
+        """Global rank of group rank ``r`` (``broadcast``'s ``src`` is a global rank)."""
+        if self.group is None or not self.enabled:
+            return r
+        return dist.get_global_rank(self.group, r)
+
     def broadcast(self, t: torch.Tensor, src: int = 0):
         if self.world == 1:
             return

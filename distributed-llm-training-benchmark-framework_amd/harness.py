@@ -31,6 +31,7 @@ from .parallel.graphs import GraphedStep, graphs_enabled
 from .ops._ext import available as ext_available, so_path
 from .comm import describe as comm_describe
 from .parallel import STRATEGIES, engine_config, make_engine
+from .parallel.ds_config import ds_precision
 from .parallel.strategy import default_config_path, load_deepspeed_config, load_fsdp_config
 from .results import make_record, print_markers, print_result, write_result
 from .utils.dist import all_reduce_max, barrier, cleanup_distributed, resolve_ranks, setup_distributed
@@ -94,7 +95,8 @@ def build_parser():
     p.add_argument("--debug-collectives", action="store_true", help="TORCH_DISTRIBUTED_DEBUG=DETAIL")
     p.add_argument("--fail-at-step", type=int, default=None, help="inject a failure (tests the suite runner)")
     p.add_argument("--timeout-min", type=int, default=30, help="collective timeout")
-    p.add_argument("--log-every", type=int, default=10)
+    p.add_argument("--log-every", type=int, default=None,
+                   help="log cadence in steps (default: the DeepSpeed config's steps_per_print, else 10)")
     p.add_argument("--no-extended", action="store_true", help="do not write the extended sidecar")
     p.add_argument("--resume", type=str, default=None, help="load a sharded checkpoint dir before training")
     p.add_argument("--save-dir", type=str, default=None, help="write a sharded checkpoint at the end (window boundary)")
@@ -132,8 +134,15 @@ def train(args):
     args.world_size, args.rank, args.local_rank = world, rank, local_rank
     auto_bucket = args.bucket_mb is None
     label = args.strategy_label or args.strategy
+    ds_cfg = None
+    if args.strategy in ("zero2", "zero3"):
+        ds_cfg = load_deepspeed_config(args.deepspeed_config or default_config_path(args.strategy))
     if args.dtype == "auto":
-        args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
+        args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else ds_precision(ds_cfg)
+    if args.log_every is None:               # DeepSpeed's steps_per_print (zero2/3.json: 10)
+        args.log_every = int((ds_cfg or {}).get("steps_per_print", 10))
+    if (ds_cfg or {}).get("wall_clock_breakdown"):
+        args.phase_timers = True             # DeepSpeed's wall-clock breakdown: per-phase HIP-event timers
     if args.grad_comm_dtype == "auto":
         args.grad_comm_dtype = "fp32" if (args.strategy == "ddp" and args.dtype == "fp16") else args.dtype
     if args.grad_comm_dtype not in ("fp32", args.dtype):
@@ -316,6 +325,8 @@ def train(args):
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
             "phase_times_ms": timers.summary() if timers is not None else None,
             "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
+            "deepspeed_config_keys": ecfg.extra.get("ds_keys") or None,
+            "config_keys_ignored": sorted((ecfg.extra.get("ds_keys") or {}).get("ignored", {})),
         }
         if is_main:
             print_result(record)

@@ -18,9 +18,11 @@ from ..ops._ext import ext
 
 class FlatAdamW:
     def __init__(self, master: torch.Tensor, segments: Sequence[Tuple[int, int, torch.Tensor]],
-                 lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01):
+                 lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, sub_group: int = 0):
         """``segments``: (owner_start, length, dst) with ``dst`` a contiguous 1-D view of length
-        ``length`` receiving the compute-dtype copy of ``master[owner_start:owner_start+length]``."""
+        ``length`` receiving the compute-dtype copy of ``master[owner_start:owner_start+length]``.
+        ``sub_group`` (DeepSpeed ZeRO-3 ``sub_group_size``, elements): update the owner space in
+        launches of at most this many elements (0: one launch)."""
         assert master.dtype == torch.float32 and master.dim() == 1
         self.master = master
         self.exp_avg = torch.zeros_like(master)
@@ -31,6 +33,8 @@ class FlatAdamW:
         self._lr_now = float(lr)
         self._tables = None
         self._seg_blocks = []    # segment -> (first, end) rows of the block tables (contiguous)
+        self.sub_group = int(sub_group or 0)
+        self._sub_ranges = None  # sub-group -> (first, end) rows of the block tables
         self.hp = None
         # compute-dtype copies written by the kernel: bf16 or fp16 (all segments share one)
         dts = {dst.dtype for _, _, dst in self.segments}
@@ -56,6 +60,9 @@ class FlatAdamW:
                 blk_seg.append(i)
                 blk_start.append(s)
             self._seg_blocks.append((first, len(blk_seg)))
+        if self.sub_group > 0:
+            per = max(1, self.sub_group // chunk)        # block-table rows per launch
+            self._sub_ranges = [(lo, min(lo + per, len(blk_seg))) for lo in range(0, len(blk_seg), per)]
         dev = self.master.device
         self._tables = (torch.tensor(blk_seg, dtype=torch.int32, device=dev),
                         torch.tensor(blk_start, dtype=torch.int64, device=dev),
@@ -89,7 +96,21 @@ class FlatAdamW:
 
     def launch(self, grad: torch.Tensor, gscale: torch.Tensor = None):
         b1, b2 = self.betas
+        if self._sub_ranges is not None and len(self._sub_ranges) > 1:
+            for lo, hi in self._sub_ranges:
+                self._launch_rows(lo, hi, grad, gscale)
+            return
         ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, *self._tables, gscale,
+                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16)
+
+    @property
+    def launches_per_step(self) -> int:
+        return len(self._sub_ranges) if self._sub_ranges else 1
+
+    def _launch_rows(self, lo, hi, grad, gscale):
+        b1, b2 = self.betas
+        ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, self._tables[0][lo:hi],
+                    self._tables[1][lo:hi], *self._tables[2:], gscale,
                     self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16)
 
     def launch_segment(self, i: int, grad: torch.Tensor, gscale: torch.Tensor = None):
@@ -98,10 +119,7 @@ class FlatAdamW:
         per-segment launches together are exactly ``launch`` -- the engine uses them to let each
         bucket's forward wait for its own parameters only."""
         lo, hi = self._seg_blocks[i]
-        b1, b2 = self.betas
-        ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, self._tables[0][lo:hi],
-                    self._tables[1][lo:hi], *self._tables[2:], gscale,
-                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16)
+        self._launch_rows(lo, hi, grad, gscale)
 
     @torch.no_grad()
     def step(self, grad: torch.Tensor, lr: float, gscale: torch.Tensor = None):
@@ -112,8 +130,12 @@ class FlatAdamW:
             self.launch(grad, gscale)
             return
         self.step_count += 1
-        ref.adamw_flat(self.master, self.exp_avg, self.exp_avg_sq, grad, lr, b1, b2, self.eps,
-                       self.weight_decay, self.step_count, gscale)
+        n = self.master.numel()
+        sg = self.sub_group if self.sub_group > 0 else n
+        for lo in range(0, n, sg):              # sub-groups: same update, launch by launch
+            hi = min(n, lo + sg)
+            ref.adamw_flat(self.master[lo:hi], self.exp_avg[lo:hi], self.exp_avg_sq[lo:hi], grad[lo:hi], lr, b1,
+                           b2, self.eps, self.weight_decay, self.step_count, gscale)
         for ostart, length, dst in self.segments:
             dst.copy_(self.master[ostart:ostart + length])
 

@@ -69,7 +69,7 @@ class FlatLayout:
 
 def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 0,
                 align: int = ALIGN, shard: bool = False, param_filter=None,
-                solo_tail: int = 0) -> FlatLayout:
+                solo_tail: int = 0, bucket_max: int = 0, solo_head: int = 0) -> FlatLayout:
     """Lay ``units`` (already in the desired memory order) out in one flat buffer.
 
     ``bucket_elems``: close a bucket once it holds at least this many elements (0 = one bucket per
@@ -79,6 +79,12 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
     units that finish last (block 0, the tied embedding): their collectives cannot overlap any
     compute, so keeping them out of a large shared bucket shortens the exposed communication tail
     (a 64 MiB bucket of blocks 2..0 + the embedding would start only after the embedding).
+    ``solo_head``: the first ``solo_head`` units get a bucket each (in backward order the LM head:
+    its collective starts right after the first backward op, and the repeated blocks behind it then
+    fill their buckets in whole groups).
+    ``bucket_max``: a hard upper bound (DeepSpeed's ``reduce_bucket_size`` / ``allgather_bucket_size``
+    semantics): a unit that would push the open bucket past it starts a new bucket.  Units are never
+    split, so a unit larger than the bound forms a bucket of its own.
     """
     slots: Dict[Tuple[int, int], ParamSlot] = {}
     buckets: List[Bucket] = []
@@ -94,8 +100,21 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
         return b.end
 
     tail_from = len(units) - max(0, int(solo_tail))
+    def unit_end(u, start):
+        """End offset of ``u``'s parameters if placed from ``start`` (same rules as below)."""
+        e = start
+        for i, p in enumerate(u.params):
+            if (param_filter is not None and not param_filter(u, i)) or id(p) in seen:
+                continue
+            e = round_up(e, align) + p.numel()
+        return e
+
     for ui, u in enumerate(units):
         if ui >= tail_from and cur is not None:
+            off = close(cur)
+            cur = None
+        if bucket_max > 0 and cur is not None and cur.end > cur.start \
+                and unit_end(u, cur.end) - cur.start > bucket_max:
             off = close(cur)
             cur = None
         placed = False
@@ -116,7 +135,7 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
         if placed:
             cur.units.append(u)
             unit_bucket[id(u)] = cur.index
-            if bucket_elems <= 0 or cur.end - cur.start >= bucket_elems or ui >= tail_from:
+            if bucket_elems <= 0 or cur.end - cur.start >= bucket_elems or ui >= tail_from or ui < solo_head:
                 off = close(cur)
                 cur = None
     if cur is not None:

@@ -37,6 +37,7 @@ import torch
 from ..ops import functional as F_
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
+from .ds_config import check_bucket_caps
 from .engine import Engine
 from .flat import ALIGN, owner_segments, plan_layout
 from .wgrad import WgradQueue
@@ -55,9 +56,13 @@ class ReplicatedEngine(Engine):
         units = list(reversed(model.units()))
         elem = torch.tensor([], dtype=self.compute_dtype).element_size()
         bucket_elems = int(cfg.bucket_mb * (1 << 20) / elem) if cfg.bucket_mb > 0 else 0
-        ds_cap = cfg.extra.get("reduce_bucket_elems")
+        # DeepSpeed's reduce_bucket_size / allgather_bucket_size (elements): hard upper bounds of one
+        # reduce-scatter / one parameter all-gather; both run per bucket here (parallel/ds_config.py)
+        caps = [int(c) for c in (cfg.extra.get("reduce_bucket_elems"), cfg.extra.get("allgather_bucket_elems")) if c]
+        ds_cap = min(caps) if caps else 0
         if ds_cap:
-            bucket_elems = min(bucket_elems, int(ds_cap)) if bucket_elems else int(ds_cap)
+            check_bucket_caps(cfg, [u.numel for u in units], cfg.strategy)
+            bucket_elems = min(bucket_elems, ds_cap) if bucket_elems else ds_cap
         # weight gradients queued and issued as strided-batched GEMMs (parallel/wgrad.py): world 1
         # flushes once per backward, world > 1 per bucket right before its collective
         self.defer_wgrad = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
@@ -68,18 +73,28 @@ class ReplicatedEngine(Engine):
         # Only the embedding (the unit that finishes last) then keeps a bucket of its own: a solo block 0
         # would be a 1-block batch (110 us) and leave 3 blocks for the group before it.
         mult = int(cfg.extra.get("bucket_unit_multiple", os.environ.get("DLTB_BUCKET_UNIT_MULTIPLE", 4)))
-        solo_tail = 2
+        solo_tail, solo_head = 2, 0
         if self.world > 1 and self.defer_wgrad and bucket_elems > 0 and mult > 1:
             sizes = sorted(u.numel for u in units)
             grp = mult * sizes[len(sizes) // 2]          # the repeated unit: a transformer block
             bucket_elems = -(-bucket_elems // grp) * grp
-            if ds_cap:
-                bucket_elems = min(bucket_elems, max(int(ds_cap), grp))
             solo_tail = 1
+            # the head (the tied 65.5 MB token table at TinyGPT-A) is a bucket of its own: otherwise it
+            # shares the first bucket with two blocks and the blocks' dW batches come out 2/4/4/4/2
+            # (a 2-block batch costs 75 us per block against 58 for 4, profiles/wgrad_batch_size_r2.txt)
+            solo_head = int(cfg.extra.get("solo_head_units", os.environ.get("DLTB_SOLO_HEAD", 1)))
         shard = self.stage >= 1
         self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
                                       solo_tail=int(cfg.extra.get("solo_tail_units",
-                                                                  os.environ.get("DLTB_SOLO_TAIL", solo_tail))))
+                                                                  os.environ.get("DLTB_SOLO_TAIL", solo_tail))),
+                                      bucket_max=ds_cap, solo_head=solo_head)
+        # DeepSpeed switches (zero2.json; all true there and by default): overlap_comm false waits
+        # for every collective where it is issued; reduce_scatter false all-reduces each bucket and
+        # keeps this rank's chunk; allgather_partitions false re-replicates the updated parameters
+        # by one broadcast per owner chunk instead of an all-gather
+        self._overlap = bool(cfg.extra.get("overlap_comm", True))
+        self._use_rs = bool(cfg.extra.get("reduce_scatter", True))
+        self._use_ag = bool(cfg.extra.get("allgather_partitions", True))
         dev, dt = self.device, self.compute_dtype
         master_full = torch.zeros(L.total, dtype=torch.float32, device=dev)
         for s in L.slots.values():
@@ -117,7 +132,7 @@ class ReplicatedEngine(Engine):
         del master_full
         self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
         self._ag_pending = {}    # bucket -> async all-gather of updated parameters (deferred step)
-        self._defer_opt = (self.stage >= 1 and self.world > 1 and
+        self._defer_opt = (self.stage >= 1 and self.world > 1 and self._overlap and
                            bool(cfg.extra.get("defer_opt", os.environ.get("DLTB_DEFER_OPT", "1") == "1")))
         self._cache_wt = True    # cached W^T of every matrix for the NT-form dgrad GEMMs (engine.py)
         self._pending = [len(b.units) for b in L.buckets]
@@ -150,7 +165,7 @@ class ReplicatedEngine(Engine):
         # embedding) reduce under the next forward instead of after the backward.  The window's
         # last micro-step drains everything before the optimizer.
         self._tail_defer = (self.stage == 2 and self.world > 1 and self.acc is not None and
-                            bool(cfg.extra.get("defer_tail_reduce", True)))
+                            self._overlap and self._use_rs and bool(cfg.extra.get("defer_tail_reduce", True)))
         self._rs_inflight = {}   # bucket -> (work, first micro-step of its window)
         self._sparse = None      # (token slot, gathered rows, gathered ids, works) of this backward
         nbytes = L.total * (4 if self.comm_f32 is not None else elem)
@@ -183,7 +198,7 @@ class ReplicatedEngine(Engine):
         if self._rs_inflight:
             b = self._bucket_of.get(id(unit))
             if b in self._rs_inflight:
-                self._drain_bucket(b)           # the previous micro-step's reduce-scatter reads this slot
+                self._drain_all()               # the previous micro-step's reduce-scatters read these slots
         s = self.layout.slot(unit, i)
         return self.flat_grad[s.offset:s.offset + s.numel].view(s.shape), self._mark(unit, i)
 
@@ -231,7 +246,11 @@ class ReplicatedEngine(Engine):
         dense table reduced after the last backward op) and every rank scatter-adds all of them
         into the reduced gradient in ``_finish_backward`` (``_apply_sparse``)."""
         b = self._bucket_of.get(id(tok[0]))
-        if self.world > 1 and b is not None and (pos is None or self._bucket_of.get(id(pos[0])) != b):
+        # the exchange happens only when the token table's unit is not the one running this backward
+        # (the tied-in-head table: its unit reported first); an untied table (Mistral) is reduced
+        # densely with its own bucket, after this backward
+        if self.world > 1 and b is not None and id(tok[0]) in self._reported \
+                and (pos is None or self._bucket_of.get(id(pos[0])) != b):
             # structurally exchanged: every micro-step (ZeRO-2) or at each window boundary
             self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(),
                                1.0 if self.stage == 2 else 1.0 / self.accum)
@@ -292,9 +311,10 @@ class ReplicatedEngine(Engine):
 
     def _launch(self, b):
         if b in self._rs_inflight:
-            self._drain_bucket(b)     # the previous micro-step's reduce-scatter of this bucket
+            self._drain_all()         # the previous micro-step's reduce-scatters (this bucket's among them)
         bk = self.layout.buckets[b]
         g = self.flat_grad[bk.start:bk.end]
+        sync = not self._overlap
         if self.stage == 0:
             if self.comm_f32 is not None:
                 c = self.comm_f32[bk.start:bk.end]
@@ -302,14 +322,18 @@ class ReplicatedEngine(Engine):
                     ext().f32_from_bf16_(c, g, False)
                 else:
                     c.copy_(g)
-                self.comm.all_reduce(c)
+                self.comm.all_reduce(c, async_op=not sync)
             else:
-                self.comm.all_reduce(g)
+                self.comm.all_reduce(g, async_op=not sync)
+        elif not self._use_rs:
+            # reduce_scatter: false -- DeepSpeed all-reduces the bucket and keeps its own partition
+            self.comm.all_reduce(g, async_op=False)
+            self.rs_out[bk.owner_start:bk.owner_start + bk.chunk].copy_(g[self.rank * bk.chunk:(self.rank + 1) * bk.chunk])
         elif self._tail_defer:
             w = self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g, track=False)
             self._rs_inflight[b] = (w, self._window_pos == 0)
         else:
-            self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g)
+            self.comm.reduce_scatter(self.rs_out[bk.owner_start:bk.owner_start + bk.chunk], g, async_op=not sync)
 
     def _drain_bucket(self, b):
         """Wait for bucket ``b``'s reduce-scatter and add its chunk into the fp32 accumulator (then
@@ -329,6 +353,27 @@ class ReplicatedEngine(Engine):
             self._apply_sparse()
 
     def _drain_all(self):
+        """Wait for every in-flight reduce-scatter and fold the chunks into the fp32 accumulator.  When
+        the whole owner space is in flight (the normal case: every bucket of the previous micro-step,
+        drained at this backward's first gradient write, a forward later), the fold is ONE launch
+        over the owner space instead of one per bucket."""
+        if not self._rs_inflight:
+            return
+        firsts = {f for _, f in self._rs_inflight.values()}
+        if len(self._rs_inflight) == len(self.layout.buckets) and len(firsts) == 1:
+            for w, _ in self._rs_inflight.values():
+                w.wait()
+            self._rs_inflight.clear()
+            first = firsts.pop()
+            if self.acc.is_cuda:
+                ext().f32_from_bf16_(self.acc, self.rs_out, not first)
+            elif first:
+                self.acc.copy_(self.rs_out)
+            else:
+                self.acc += self.rs_out
+            if self._sparse is not None:
+                self._apply_sparse()
+            return
         for b in sorted(self._rs_inflight):
             self._drain_bucket(b)
 
@@ -347,6 +392,9 @@ class ReplicatedEngine(Engine):
                 self._launch(b)
         self._phase("comm_wait_begin")
         self._wait_works()
+        if self._tail_defer and self._is_boundary:
+            self._drain_all()                   # the optimizer reads the window's full sum next (one
+            #                                     fold launch; the token rows are applied in it)
         if self._sparse is not None and not (self._tail_defer and not self._is_boundary and _SPARSE_DEFER):
             b = self._bucket_of[id(self._sparse[0][0])]
             if b in self._rs_inflight:
@@ -355,8 +403,6 @@ class ReplicatedEngine(Engine):
                 self._apply_sparse()
         # (ZeRO-2 inside a window: the row all-gathers stay in flight with the table's reduce-
         # scatter and are applied when that bucket is drained, under the next forward)
-        if self._tail_defer and self._is_boundary:
-            self._drain_all()                   # the optimizer reads the window's full sum next
         self._phase("comm_wait_end")
         self._pending = [len(b.units) for b in self.layout.buckets]
         self._next = 0
@@ -382,11 +428,26 @@ class ReplicatedEngine(Engine):
 
     def _deferred_optimizer_step(self, lr):
         self._update(lr)
+        if not self._use_ag:
+            self._regather(async_op=False)
+            return
         for b in reversed(range(len(self.layout.buckets))):     # forward order: embedding first
             bk = self.layout.buckets[b]
             full = self.flat_param[bk.start:bk.end]
             mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
             self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
+
+    def _regather(self, async_op=True):
+        """Re-replicate the updated parameter chunks: an all-gather per bucket, or (DeepSpeed's
+        ``allgather_partitions: false``) one broadcast per owner chunk."""
+        for bk in self.layout.buckets:
+            full = self.flat_param[bk.start:bk.end]
+            if self._use_ag:
+                mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
+                self.comm.all_gather(full, mine, async_op=async_op)
+            else:
+                for r in range(self.world):
+                    self.comm.broadcast(full[r * bk.chunk:(r + 1) * bk.chunk], src=self.comm.global_rank(r))
 
     def _wait_param_gathers(self):
         self._drain_all()
@@ -398,19 +459,13 @@ class ReplicatedEngine(Engine):
         # (ZeRO-1 reduce-scattered its window-accumulated gradients during the boundary backward)
         self._update(lr)
         if self.stage >= 1 and self.world > 1:
-            for bk in self.layout.buckets:
-                full = self.flat_param[bk.start:bk.end]
-                mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
-                self.comm.all_gather(full, mine)
+            self._regather()
             self._wait_works()
 
     def _after_param_load(self):
         self._wt_epoch = -1                  # cached transposes are stale
         if self.stage >= 1 and self.world > 1:   # other ranks' owner parts
-            for bk in self.layout.buckets:
-                full = self.flat_param[bk.start:bk.end]
-                mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
-                self.comm.all_gather(full, mine, async_op=False)
+            self._regather(async_op=False)
 
     # ------------------------------------------------------------------ introspection
     def memory_report(self):

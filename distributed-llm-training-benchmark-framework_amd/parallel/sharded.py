@@ -151,12 +151,30 @@ class ShardedEngine(Engine):
             segs.append((0, p_chunk, self.p_flat[self.rank * p_chunk:(self.rank + 1) * p_chunk]))
         if owner > p_chunk:
             segs.append((p_chunk, owner - p_chunk, self.shard_buf))
-        self.opt = FlatAdamW(master, segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
+        self.opt = FlatAdamW(master, segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay,
+                             sub_group=int(cfg.extra.get("sub_group_elems", 0)))
         self.rs_out = torch.zeros(owner, dtype=dt, device=dev)
         self.acc = torch.zeros(owner, dtype=torch.float32, device=dev) if (self.accum > 1 and self.world > 1) else None
         total_sharded = sum(g.total for g in groups)
         self.keep_all = bool(cfg.max_live_parameters) and total_sharded <= cfg.max_live_parameters and \
             total_sharded <= (cfg.max_reuse_distance or _HUGE)
+        # ZeRO-3 (parallel/ds_config.py): stage3_prefetch_bucket_size is an element budget of units
+        # gathered ahead; without one (FSDP) ``cfg.prefetch`` units are.  A unit gathered for the
+        # forward is kept for its backward when the parameters touched in between (the later units'
+        # forward and backward) stay within stage3_max_reuse_distance and the gathered total within
+        # stage3_max_live_parameters (DeepSpeed's release rule), instead of released and re-gathered
+        self._prefetch_elems = int(cfg.extra.get("prefetch_elems", 0)) if cfg.zero_stage == 3 else 0
+        self._reuse_keep = set()
+        if cfg.zero_stage == 3 and not self.keep_all and cfg.max_reuse_distance:
+            after = 0
+            for g in reversed(order):
+                if 2 * after <= cfg.max_reuse_distance:
+                    self._reuse_keep.add(g.gid)
+                after += g.total
+        self._overlap = bool(cfg.extra.get("overlap_comm", True))
+        if cfg.zero_stage == 3 and cfg.extra.get("reduce_bucket_elems"):
+            from .ds_config import check_bucket_caps
+            check_bucket_caps(cfg, [g.total for g in groups] + [p_total], "zero3")   # (+ the persistent block)
         self._p_pending = len([u for u in self.model.units()
                                if any(self._persistent(u, i) for i in range(len(u.params)))])
         self._p_left = self._p_pending
@@ -306,10 +324,23 @@ class ShardedEngine(Engine):
 
     def _prefetch(self, g, direction):
         k = self._pos[g.gid]
+        if self._prefetch_elems > 0:
+            budget, kk = self._prefetch_elems, k + direction
+            while 0 <= kk < len(self._order):
+                nxt = self._order[kk]
+                if budget < nxt.total and kk != k + direction:
+                    break                            # (the next unit is always prefetched)
+                budget -= nxt.total
+                self._launch_gather(nxt)
+                kk += direction
+            return
         for j in range(1, max(0, int(self.cfg.prefetch)) + 1):
             kk = k + direction * j
             if 0 <= kk < len(self._order):
                 self._launch_gather(self._order[kk])
+
+    def _live(self) -> int:
+        return sum(g.total for g in self.groups if g.full is not None)
 
     # ------------------------------------------------------------------ runtime interface
     def acquire(self, unit):
@@ -325,7 +356,8 @@ class ShardedEngine(Engine):
         if g.fwd_left == 0:
             g.fwd_left = len(g.units)
             if self.model.training and self.cfg.reshard_after_forward and not g.root and not self.keep_all:
-                self._release(g)
+                if not (g.gid in self._reuse_keep and self._live() <= self.cfg.max_live_parameters):
+                    self._release(g)
 
     def acquire_tied(self, unit):
         """Parameters of another unit used by a tied consumer (lm_head = wte): no prefetch, no
@@ -411,7 +443,8 @@ class ShardedEngine(Engine):
         unit, i = tok
         persistent = (id(unit), i) in self.p_layout.slots
         done = self._p_reduced if persistent else self._group_of[id(unit)].gid in self._reduced
-        if self.world > 1 and not persistent and (pos is None or self._group_of[id(pos[0])] is not self._group_of[id(unit)]):
+        if self.world > 1 and not persistent and id(unit) in self._reported \
+                and (pos is None or self._group_of[id(pos[0])] is not self._group_of[id(unit)]):
             self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(), 1.0)
         if self.world == 1 or not done:
             return super().embedding_backward(tok, pos, dx, idx, p, seed, site)
@@ -456,7 +489,7 @@ class ShardedEngine(Engine):
         self._reduced.add(g.gid)
         if self.world > 1:
             out = self.rs_out[g.owner_start:g.owner_start + g.chunk]
-            self.comm.reduce_scatter(out, g.grad)
+            self.comm.reduce_scatter(out, g.grad, async_op=self._overlap)
             self._held_grads.append(g.grad)
         g.grad = None
 
@@ -539,7 +572,14 @@ class ShardedEngine(Engine):
         return {"shard_param_bytes": self.shard_buf.numel() * e, "persistent_param_bytes": self.p_flat.numel() * e,
                 "optimizer_bytes": self.opt.state_bytes, "groups": len(self.groups),
                 "largest_group_mb": round(max(g.total for g in self.groups) * e / 2**20, 2),
-                "keep_all_gathered": self.keep_all}
+                "keep_all_gathered": self.keep_all,
+                # speed-for-HBM buffers beyond DeepSpeed / torch FSDP's footprint (models < 2B params,
+                # world > 1): full-size per-group gradient buffers reused every micro-step, and the
+                # per-window W^T copies of the NT-form data-gradient GEMMs.  peak_vram_gb includes them.
+                "resident_grad_bytes": sum(g.grad_buf.numel() * e for g in self.groups
+                                           if g.grad_buf is not None and self.world > 1),
+                "weight_t_cache_bytes": sum(t.numel() * t.element_size() for t, _ in (self._wt_multi or {}).values()),
+                "gather_pool_bytes": sum(b.numel() * e for bufs in self._gpool.values() for b in bufs)}
 
     def full_state_dict(self):
         out = {}

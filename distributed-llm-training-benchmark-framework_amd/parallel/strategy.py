@@ -13,12 +13,12 @@ Step semantics (``--accum-semantics``):
   uniform — every strategy gets the ZeRO semantics (accumulation + clipping + schedule).
 """
 import json
-import math
 import os
 from typing import Optional
 
 import torch
 
+from .ds_config import apply_deepspeed_config
 from .engine import EngineConfig
 from .replicated import DDPEngine, Zero2Engine
 from .sharded import FSDPEngine, Zero3Engine
@@ -33,12 +33,6 @@ def default_config_path(strategy: str) -> Optional[str]:
     if strategy == "fsdp":
         return os.path.join(_ROOT, "configs", "fsdp", "fsdp_config.yaml")
     return None
-
-
-def _num(v, default=None):
-    if v is None or v == "auto":
-        return default
-    return float(v) if not isinstance(v, bool) else v
 
 
 def load_deepspeed_config(path: str) -> dict:
@@ -69,37 +63,29 @@ def engine_config(strategy: str, grad_accum: int = 1, semantics: str = "referenc
         raise ValueError(f"unknown strategy {strategy}")
     cfg = EngineConfig(strategy=strategy, compute_dtype=compute_dtype, bucket_mb=bucket_mb, seed=seed)
     ds = ds_config or {}
-    opt = (ds.get("optimizer") or {}).get("params", {})
     zero_like = strategy in ("zero2", "zero3") or semantics == "uniform"
     if zero_like:
-        cfg.lr = _num(opt.get("lr"), 1e-4)
-        cfg.betas = tuple(opt.get("betas", (0.9, 0.999)))
-        cfg.eps = _num(opt.get("eps"), 1e-8)
-        cfg.weight_decay = _num(opt.get("weight_decay"), 0.01)
+        # defaults = the reference's DeepSpeed configs; the DS JSON (if any) overrides them below
+        cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay = 1e-4, (0.9, 0.999), 1e-8, 0.01
         cfg.grad_accum = max(1, int(grad_accum))
-        cfg.grad_clip = _num(ds.get("gradient_clipping"), 1.0 if not ds else 0.0)
-        sched = ds.get("scheduler")
-        if sched is None and not ds:
-            sched = {"type": "WarmupLR", "params": {"warmup_min_lr": 0, "warmup_max_lr": cfg.lr,
-                                                    "warmup_num_steps": 5}}
-        cfg.scheduler = sched
+        cfg.grad_clip = 1.0 if not ds else 0.0
+        cfg.scheduler = None if ds else {"type": "WarmupLR", "params": {
+            "warmup_min_lr": 0, "warmup_max_lr": cfg.lr, "warmup_num_steps": 5}}
     else:   # reference DDP / FSDP: AdamW(lr=1e-4, wd=0.01) every micro-step
         cfg.lr, cfg.weight_decay, cfg.grad_accum, cfg.grad_clip, cfg.scheduler = 1e-4, 0.01, 1, 0.0, None
-    z = ds.get("zero_optimization", {}) or {}
     if strategy == "zero2":
-        cfg.zero_stage = int(z.get("stage", 2)) if int(z.get("stage", 2)) in (1, 2) else 2
+        cfg.zero_stage = 2
+    if strategy == "zero3":
+        cfg.zero_stage = 3
+        cfg.persistence_threshold, cfg.max_live_parameters, cfg.max_reuse_distance = int(1e5), int(1e9), int(1e9)
+        cfg.extra["prefetch_elems"] = int(5e8)
+    # every DeepSpeed key is honoured, satisfied by construction, or rejected (parallel/ds_config.py)
+    cfg.extra["ds_keys"] = apply_deepspeed_config(cfg, ds, strategy, zero_like) if ds else {}
+    if strategy == "zero2":
         if grad_reduce == "window":
             cfg.zero_stage = 1
         cfg.extra["grad_reduce"] = "window" if cfg.zero_stage == 1 else "micro"
-        rb = _num(z.get("reduce_bucket_size"))
-        if rb:
-            cfg.extra["reduce_bucket_elems"] = int(rb)
     if strategy == "zero3":
-        cfg.zero_stage = 3
-        cfg.persistence_threshold = int(_num(z.get("stage3_param_persistence_threshold"), 1e5))
-        cfg.max_live_parameters = int(_num(z.get("stage3_max_live_parameters"), 1e9))
-        cfg.max_reuse_distance = int(_num(z.get("stage3_max_reuse_distance"), 1e9))
-        cfg.prefetch = 1 if _num(z.get("stage3_prefetch_bucket_size"), 5e8) > 0 else 0
         cfg.reshard_after_forward = True
         cfg.wrap = "unit"
     if strategy == "fsdp":

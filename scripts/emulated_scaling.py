@@ -30,6 +30,9 @@ STRATS = {
     "fsdp_root": ["--strategy", "fsdp", "--fsdp-wrap", "root"],
     "zero2": ["--strategy", "zero2"],
     "zero3": ["--strategy", "zero3"],
+    # BASELINE configs #2 / #3 name DDP and FSDP full-shard in bf16
+    "ddp_bf16": ["--strategy", "ddp", "--dtype", "bf16"],
+    "fsdp_bf16": ["--strategy", "fsdp", "--dtype", "bf16"],
 }
 
 

@@ -47,6 +47,14 @@ CASES = {
 EXTRA_CASES = {
     "zero3_m7b": dict(strategy="zero3", tier="m7b_2l", persist=100_000),
     "dropout": dict(strategy="zero2", dropout=0.1, same_rows=True),
+    # DeepSpeed switches (parallel/ds_config.py): overlap_comm / reduce_scatter / allgather_partitions
+    # false -> synchronous collectives, all-reduce + own chunk, per-owner broadcasts
+    "zero2_ds_switches": dict(strategy="zero2", extra={"overlap_comm": False, "reduce_scatter": False,
+                                                       "allgather_partitions": False}),
+    # ZeRO-3 with an element prefetch budget (several units ahead), the reuse-distance keep of the
+    # last units (not all: reuse distance below the model size) and AdamW sub-groups
+    "zero3_ds_budgets": dict(strategy="zero3", extra={"prefetch_elems": 1_700_000, "sub_group_elems": 300_000},
+                             over={"max_live_parameters": 10**9, "max_reuse_distance": 2_200_000}),
 }
 
 
@@ -79,9 +87,11 @@ def run_case(name, spec, world, rank, device, a):
         over["max_live_parameters"] = 0          # release after use: exercise every re-gather
         if "persist" in spec:
             over["persistence_threshold"] = spec["persist"]
+    over.update(spec.get("over", {}))
     cfg = engine_config(spec["strategy"], a.accum, "uniform", None, fc, bucket_mb=a.bucket_mb,
                         overrides=over, grad_reduce=spec.get("grad_reduce", "micro"))
     cfg.extra["grad_comm_dtype"] = spec.get("grad_comm_dtype", "compute")
+    cfg.extra.update(spec.get("extra", {}))
     eng = make_engine(model, cfg, device)
     eng.train()
     g = torch.Generator().manual_seed(123)

@@ -94,3 +94,37 @@ def test_record_markers_roundtrip(capsys):
     out = capsys.readouterr().out
     assert ("=" * 80) in out
     assert extract_from_log(out) == dict(rec)
+
+
+def test_emulated_suite_labels_predictions(tmp_path):
+    """scripts/emulated_suite.py: every predicted series is labelled ``<strategy>_pred`` in
+    result.json and metrics.csv, each row says whether it is a prediction, grad_accum is the CLI
+    value (4, as the harness writes it) even where the engine's accumulation is 1, and the bf16
+    DDP row gets its own series (BASELINE config #2)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    recs = []
+    for strat, dtype, ws, ms in (("ddp", "fp16", 1, 8.0), ("ddp", "fp16", 8, 10.0), ("ddp", "bf16", 1, 7.5),
+                                 ("ddp", "bf16", 8, 9.0), ("zero2", "bf16", 1, 7.0), ("zero2", "bf16", 8, 8.5)):
+        rec = {"metric": "tokens_per_sec", "n_gpus": 1 if ws > 1 else ws, "steps": 20, "ms_per_step": ms,
+               "value": 2048 * ws / ms * 1e3, "dtype": dtype, "mean_loss": 10.0, "peak_hbm_gb": 5.0,
+               "config": {"model": "TinyGPT-A", "seq_len": 2048, "micro_batch_per_gpu": 1,
+                          "grad_accum": 1 if strat == "ddp" else 4, "parallelism": f"{strat}-dp{ws}"}}
+        if ws > 1:
+            rec.update(prediction=True, emulated_world=ws, peak_hbm_gb_per_rank=4.0)
+        recs.append(rec)
+    src = tmp_path / "pred.jsonl"
+    src.write_text("\n".join(json.dumps(r) for r in recs) + "\n")
+    out = tmp_path / "emu"
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "emulated_suite.py"), str(src), str(out)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    df = pd.read_csv(out / "summary" / "metrics.csv")
+    assert set(df["strategy"]) == {"ddp_pred", "ddp_bf16_pred", "zero2_pred"}
+    assert list(df["prediction"]) == [ws > 1 for ws in df["world_size"]]
+    assert (df["grad_accum"] == 4).all()
+    z8 = df[(df.strategy == "zero2_pred") & (df.world_size == 8)].iloc[0]
+    assert abs(z8["scaling_efficiency_pct"] - 100 * 7.0 / 8.5) < 0.01       # vs its measured WS=1 row
+    res = json.loads((out / "bench-master-zero2_pred-ws8-seq2048_results" / "result.json").read_text())
+    assert res["prediction"] is True and res["emulated_world"] == 8

@@ -21,7 +21,7 @@ import torch
 
 import dltb  # noqa: F401
 from dltb.comm import Comm
-from dltb.models import get_model_config
+from dltb.models import build_model, get_model_config
 from dltb.models.tinygpt import TinyGPT
 from dltb.parallel import engine_config, make_engine
 
@@ -61,7 +61,7 @@ def _cfg(strategy, accum, **kw):
     ds = None
     if strategy in ("zero2", "zero3"):
         ds = {"gradient_clipping": 1.0, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3}},
-              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 2000,
+              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 5e8,
                                     "stage3_param_persistence_threshold": 300,
                                     "stage3_max_live_parameters": kw.pop("max_live", 1e9),
                                     "stage3_max_reuse_distance": 1e9}}
@@ -78,21 +78,26 @@ CASES = [
     ("fsdp", 1, {"fsdp": {"auto_wrap_policy": "size_based"}}),
     ("fsdp", 1, {"fsdp": {"sharding_strategy": "shard_grad_op"}}),
     ("fsdp", 2, {"semantics": "uniform"}),
+    # Mistral shape: untied token table, reduced densely with the embedding's own bucket / group
+    ("ddp", 1, {"tier": "mtiny"}), ("zero2", 4, {"tier": "mtiny"}), ("zero3", 4, {"tier": "mtiny"}),
 ]
 
 
 @pytest.mark.parametrize("strategy,accum,kw", CASES, ids=[f"{c[0]}-{i}" for i, c in enumerate(CASES)])
 def test_wire_bytes_equal_model(emulate4, strategy, accum, kw):
     torch.manual_seed(0)
-    model = TinyGPT(get_model_config("tiny", 16, dropout=0.0))
-    eng = make_engine(model, _cfg(strategy, accum, **dict(kw)), "cpu")
+    kw = dict(kw)
+    mcfg = get_model_config(kw.pop("tier", "tiny"), 16)
+    mcfg.dropout = 0.0
+    model = build_model(mcfg)
+    eng = make_engine(model, _cfg(strategy, accum, **kw), "cpu")
     eng.train()
     assert eng.world == 4
     g = torch.Generator().manual_seed(1)
 
     def window():
         for _ in range(accum):
-            x = torch.randint(0, 128, (1, 16), generator=g)
+            x = torch.randint(0, min(128, mcfg.vocab_size), (1, 16), generator=g)
             loss = eng(x, x)[1]
             eng.backward(loss)
             eng.step()

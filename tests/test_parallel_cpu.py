@@ -49,7 +49,7 @@ def _cfg(strategy, accum, semantics="reference", **kw):
     if strategy in ("zero2", "zero3"):
         ds = {"gradient_clipping": 1.0, "optimizer": {"type": "AdamW", "params": {"lr": 1e-3, "weight_decay": 0.01}},
               "scheduler": {"type": "WarmupLR", "params": {"warmup_min_lr": 0, "warmup_max_lr": 1e-3, "warmup_num_steps": 3}},
-              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 2000,
+              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 5e8,
                                     "stage3_param_persistence_threshold": 300,
                                     "stage3_max_live_parameters": kw.pop("max_live", 1e9),
                                     "stage3_max_reuse_distance": 1e9}}

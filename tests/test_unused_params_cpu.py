@@ -116,7 +116,7 @@ def _cfg(strategy, accum, semantics="reference", stage=None):
     if strategy in ("zero2", "zero3"):
         ds = {"gradient_clipping": 1.0,
               "optimizer": {"type": "AdamW", "params": {"lr": 1e-2, "weight_decay": 0.01}},
-              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 2000,
+              "zero_optimization": {"stage": 2 if strategy == "zero2" else 3, "reduce_bucket_size": 5e8,
                                     "stage3_param_persistence_threshold": 100,
                                     "stage3_max_live_parameters": 0, "stage3_max_reuse_distance": 1e9}}
     c = engine_config(strategy, accum, semantics, ds, None, bucket_mb=0.0005)
