@@ -235,9 +235,10 @@ def run_rank(args) -> int:
         wire_timed = engine.comm.wire_bytes()      # the timed steps' collectives (before finalize)
         opt_steps = engine.opt_steps - opt0
         comm_model_ms = engine.comm.modelled_us() / 1e3 / max(1, args.steps) if args.emulate else None
-        host_ms = None
+        host_ms = host_note = None
         if args.host_check and cuda:
-            host_ms = host_enqueue_ms(one_step, min(args.steps, 6), device)
+            host_ms, host_note = host_enqueue_ms(one_step, min(args.steps, 6), device,
+                                                 step_ms=elapsed / max(1, args.steps) * 1e3)
         engine.finalize()                    # a deferred update of the last window: outside the timed region
         mean_loss = float(loss_hist[:args.steps].mean().item()) if args.steps else 0.0
         final_loss = float(loss.item())
@@ -324,6 +325,8 @@ def run_rank(args) -> int:
                                    for op, (a, b, src) in engine.comm.emu_params.items()
                                    if op in ("all_reduce", "reduce_scatter", "all_gather")},
                     "emu_channels": engine.comm.emu_channels,
+                    "emu_hbm_passes": engine.comm.emu_pass_of,
+                    "emu_host_us_per_call": engine.comm.emu_host_us,
                     "comm_model_ms_per_step": comm_model_ms,
                     "vs_baseline": None, "vs_baseline_per_gpu": None,
                     "predicted_ms_per_step": ms,
@@ -332,6 +335,7 @@ def run_rank(args) -> int:
             if host_ms is not None:
                 out["host_enqueue_ms_per_step"] = host_ms
                 out["host_over_gpu"] = host_ms / ms if ms else None
+                out["host_check_note"] = host_note
             print(json.dumps(out), flush=True)
         if cuda:
             from dltb.utils.gemm_tuning import flush_tunableop
@@ -341,13 +345,17 @@ def run_rank(args) -> int:
         cleanup_distributed()
 
 
-def host_enqueue_ms(one_step, k, device):
+def host_enqueue_ms(one_step, k, device, step_ms=0.0):
     """Host time to enqueue ``k`` eager micro-steps while the GPU is held busy by one long wait
-    kernel in front of them (so no launch waits for the GPU): the host cost per step.  A step that
-    synchronises with the GPU would show as ~the hold time."""
+    kernel in front of them (so no launch waits for the GPU): the host cost per step.  The hold
+    lasts at least 3 x the GPU time of the k steps, so the enqueue never outlasts it while the host
+    is ahead.  Returns (ms per step, note): the note flags a run whose enqueue still reached the
+    hold -- a host sync in the step, or the launch queue full (the runtime blocks the host once its
+    hardware queues hold that many packets) -- in which case the ratio is a lower bound of nothing
+    and must not be read as host cost."""
     import torch
     from dltb.ops._ext import ext
-    hold_us = 3e5 + 5e4 * k
+    hold_us = max(3e5 + 5e4 * k, 3.0 * k * step_ms * 1e3)
     for _ in range(2):      # the first pass grows the allocator's cache: blocks still recorded on a
         torch.cuda.synchronize(device)     # collective stream cannot be reused while the GPU is held
         ext().comm_emu(None, 1, None, None, 1.0, 1, 0, hold_us, 0.0, 1, 0)   # one paced wave: GPU busy
@@ -357,9 +365,12 @@ def host_enqueue_ms(one_step, k, device):
         t1 = time.perf_counter()
         torch.cuda.synchronize(device)
     ms = (t1 - t0) / k * 1e3
+    note = f"hold {hold_us / 1e3:.0f} ms for {k} steps"
     if ms * k * 1e3 > 0.9 * hold_us:
-        print(f"[host-check] enqueue took {ms * k:.1f} ms: a step waits for the GPU (host sync)", flush=True)
-    return ms
+        note += "; INVALID: the enqueue reached the hold (host sync or launch queue full)"
+        print(f"[host-check] enqueue took {ms * k:.1f} ms of a {hold_us / 1e3:.0f} ms hold: a step waits for "
+              "the GPU (host sync or full launch queue)", flush=True)
+    return ms, note
 
 
 def main(argv=None):

@@ -42,6 +42,7 @@ engines own their communication, and this module is the one place that talks to
   synchronous or racy, and only RCCL on several GPUs runs truly asynchronously).
 """
 import os
+import time
 from collections import OrderedDict
 
 import torch
@@ -123,6 +124,9 @@ class _Lazy:
 
 _REDUCE_OPS = {"sum": "SUM", "max": "MAX", "min": "MIN", "avg": "AVG"}
 
+# emulated fabric: local HBM passes over the full buffer per collective (see Comm.__init__)
+EMU_HBM_PASSES = {"reduce_scatter": 3, "all_gather": 2, "all_reduce": 5, "broadcast": 2, "all_to_all": 2}
+
 
 def ring_factor(op: str, world: int) -> float:
     """Bytes one rank sends per byte of the (full) buffer, ring algorithms."""
@@ -145,9 +149,19 @@ class Comm:
             self.world, self.rank, self.backend = self.emulate, int(os.environ.get("DLTB_EMU_RANK", "0")), "emulate"
             if not 0 <= self.rank < self.world:
                 raise ValueError(f"DLTB_EMU_RANK={self.rank} outside emulate:{self.world}")
-            from .topology import measured_params
+            from .topology import measured_params, pg_host_cost_us
             self.emu_channels = int(os.environ.get("DLTB_EMU_CHANNELS", "32"))
-            self.emu_passes = int(os.environ.get("DLTB_EMU_HBM_PASSES", "1"))
+            # local HBM passes over the full buffer per op (ring algorithms, N ranks): reduce-scatter
+            # reads its input and writes + re-reads every received chunk (~3), all-gather writes and
+            # re-reads the forwarded chunks (~2), all-reduce is both (~5).  DLTB_EMU_HBM_PASSES
+            # overrides every op (0: no traffic stream -- the N-rank code path alone)
+            env_p = os.environ.get("DLTB_EMU_HBM_PASSES")
+            self.emu_pass_of = {op: (int(env_p) if env_p is not None else n) for op, n in EMU_HBM_PASSES.items()}
+            self.emu_passes = max(self.emu_pass_of.values())      # (reported; 0 only if all are)
+            # host time of the ProcessGroupNCCL call each emulated collective stands in for
+            # (profiles/pg_host_cost.json, scripts/probes/pg_host_cost.py); spun on the host before
+            # the paced kernel is launched, so an eager emulated step pays what a real one would
+            self.emu_host_us = pg_host_cost_us()
             self.emu_params = {}          # op -> (alpha_us, bus_GBps, source)
             for op in ("all_reduce", "reduce_scatter", "all_gather", "broadcast", "all_to_all"):
                 a, b, src = measured_params(self.world, "all_reduce" if op == "all_reduce" else "reduce_scatter")
@@ -232,9 +246,15 @@ class Comm:
         side = self._emu_stream
         side.wait_stream(torch.cuda.current_stream(full.device))   # starts after its producers
         alpha, beta = self._emu_time(op, full)
+        host = self.emu_host_us.get(op, 0.0)
+        if host > 0:                          # the ProcessGroupNCCL call's host time
+            t_end = time.perf_counter() + host * 1e-6
+            while time.perf_counter() < t_end:
+                pass
+        passes = self.emu_pass_of.get(op, 1)
         # (DLTB_EMU_HBM_PASSES=0: no traffic stream, the numerics stand-in only -- isolates the
         # N-rank code path from the collectives' HBM contention)
-        ext().comm_emu(full if self.emu_passes > 0 else None, max(1, self.emu_passes), dst, src, float(scale),
+        ext().comm_emu(full if passes > 0 else None, max(1, passes), dst, src, float(scale),
                        int(replicas), int(rep_stride), float(alpha), float(beta), self.emu_channels,
                        self._emu_handle)
         keep = (full, dst, src)

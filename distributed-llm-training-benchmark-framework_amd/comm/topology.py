@@ -144,6 +144,32 @@ def calibrate_fabric(device, sizes_mb=(4, 16, 64), iters: int = 5, dtype=None, g
     return {"world": world, "rows": rows, "fits": fits}
 
 
+DEFAULT_PG_HOST_US = {"reduce_scatter": 20.0, "all_gather": 20.0, "all_reduce": 20.0, "broadcast": 20.0,
+                      "all_to_all": 20.0}
+PG_HOST_PROFILE = os.path.join(_ROOT, "profiles", "pg_host_cost.json")
+
+
+def pg_host_cost_us(path: str = None) -> dict:
+    """Host microseconds of one ProcessGroupNCCL call per op (issue + wait), measured by
+    scripts/probes/pg_host_cost.py on the real RCCL library (``profiles/pg_host_cost.json``);
+    ``$DLTB_EMU_HOST_US`` overrides every op (0 disables), else DEFAULT_PG_HOST_US."""
+    env = os.environ.get("DLTB_EMU_HOST_US")
+    if env is not None:
+        return {op: float(env) for op in DEFAULT_PG_HOST_US}
+    out = dict(DEFAULT_PG_HOST_US)
+    try:
+        with open(path or os.environ.get("DLTB_PG_HOST_PROFILE") or PG_HOST_PROFILE) as f:
+            per = json.load(f)["per_op_us"]
+        for op in out:
+            if op in per:
+                out[op] = float(per[op])
+        out["broadcast"] = out["all_gather"]
+        out["all_to_all"] = out["all_gather"]
+    except (OSError, ValueError, KeyError, TypeError):
+        pass
+    return out
+
+
 def recommend_bucket_mb(world: int, overhead: float = 0.2, bus_gbps: float = None,
                         alpha_us: float = None, op: str = "reduce_scatter") -> float:
     """Smallest power-of-two MiB bucket with alpha <= overhead x transfer time, alpha and bus

@@ -168,6 +168,15 @@ class ReplicatedEngine(Engine):
                             self._overlap and self._use_rs and bool(cfg.extra.get("defer_tail_reduce", True)))
         self._rs_inflight = {}   # bucket -> (work, first micro-step of its window)
         self._sparse = None      # (token slot, gathered rows, gathered ids, works) of this backward
+        # ZeRO-2 per-micro-step reduce-scatter, inside a window: the token rows of micro-step m's
+        # embedding backward are not exchanged; they are scatter-added into micro-step m+1's dense
+        # token-table gradient (after the head's dW, before its bucket's reduce-scatter).  The
+        # window's sum is unchanged (the reduce-scatter is linear); only the window's last micro-step
+        # exchanges its rows.  2048 rows scattered locally instead of an all-gather of world x 2048
+        # rows + ids and a sort-path scatter every micro-step.
+        self._carry_on = (self._tail_defer and
+                          bool(cfg.extra.get("carry_token_rows", os.environ.get("DLTB_CARRY_ROWS", "1") == "1")))
+        self._carry = None       # (token slot, rows, ids) waiting for the next micro-step's head
         nbytes = L.total * (4 if self.comm_f32 is not None else elem)
         if self.world > 1:
             # modelled wire bytes one rank sends per micro-step (ring algorithms): DDP one all-reduce
@@ -223,6 +232,8 @@ class ReplicatedEngine(Engine):
 
     def grads_ready(self, unit):
         self._reported.add(id(unit))
+        if self._carry is not None and self._carry[0][0] is unit:
+            self._apply_carry()
         b = self._bucket_of.get(id(unit))
         if b is None:
             return
@@ -251,9 +262,10 @@ class ReplicatedEngine(Engine):
         # densely with its own bucket, after this backward
         if self.world > 1 and b is not None and id(tok[0]) in self._reported \
                 and (pos is None or self._bucket_of.get(id(pos[0])) != b):
-            # structurally exchanged: every micro-step (ZeRO-2) or at each window boundary
+            # structurally exchanged: every micro-step (ZeRO-2), at each window boundary (ZeRO-1, DDP
+            # windows, and ZeRO-2 carrying the rows of the window's other micro-steps)
             self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(),
-                               1.0 if self.stage == 2 else 1.0 / self.accum)
+                               1.0 if (self.stage == 2 and not self._carry_on) else 1.0 / self.accum)
         if self.world == 1 or b is None or not (self._reduce_now() and b < self._next):
             return super().embedding_backward(tok, pos, dx, idx, p, seed, site)
         d = dx.shape[-1]
@@ -262,11 +274,22 @@ class ReplicatedEngine(Engine):
         if pos is not None:
             dwpe, acc_p = self.grad_slot(*pos)
             F_.embed_bwd(dx, idx, None, dwpe, acc_p, p, seed, site)
+        if self._carry_on and not self._is_boundary:
+            self._carry = (tok, rows, idx.reshape(1, -1).clone())
+            return
         rows_all = rows.new_empty((self.world * rows.shape[0], d))
         idx_all = idx.new_empty((self.world * idx.shape[0], idx.shape[1]))
         works = [self.comm.all_gather(rows_all, rows, track=False),
                  self.comm.all_gather(idx_all.view(-1), idx.reshape(-1).contiguous(), track=False)]
         self._sparse = (tok, rows_all, idx_all, works)
+
+    def _apply_carry(self):
+        """The previous micro-step's token rows, scatter-added into this micro-step's dense token-table
+        gradient (written by the head's dW GEMM, already queued on the stream)."""
+        tok, rows, ids = self._carry
+        self._carry = None
+        s = self.layout.slot(*tok)
+        F_.embed_bwd(rows, ids, self.flat_grad[s.offset:s.offset + s.numel].view(s.shape), None, False, 0.0, None, 0)
 
     def _apply_sparse(self):
         """Scatter-add the gathered token rows into the reduced token-table gradient: DDP into the

@@ -193,6 +193,12 @@ class ShardedEngine(Engine):
         self._reduced = set()        # group ids reduce-scattered in this micro-step
         self._p_reduced = False      # the persistent block reduce-scattered in this micro-step
         self._sparse = None          # (token slot, persistent?, gathered rows, gathered ids, works)
+        # inside an accumulation window the token rows are carried into the next micro-step's dense
+        # head-group gradient instead of exchanged (as the replicated engines do; the window's sum is
+        # unchanged); only the window's last micro-step exchanges them
+        self._carry_on = (self.world > 1 and self.accum > 1 and
+                          bool(cfg.extra.get("carry_token_rows", os.environ.get("DLTB_CARRY_ROWS", "1") == "1")))
+        self._carry = None
         # single process: the dW products of all blocks run as strided-batched GEMMs at the end of
         # backward (parallel/wgrad.py); with shards, each group's gradient is reduce-scattered the
         # moment it is complete, so they are issued immediately
@@ -423,6 +429,11 @@ class ShardedEngine(Engine):
 
     def grads_ready(self, unit):
         self._reported.add(id(unit))
+        if self._carry is not None and self._carry[0][0] is unit:
+            from ..ops import functional as F_
+            tok, rows, ids = self._carry
+            self._carry = None
+            F_.embed_bwd(rows, ids, self.grad_slot(*tok)[0], None, False, 0.0, None, 0)
         g = self._group_of[id(unit)]
         if any(self._persistent(unit, i) for i in range(len(unit.params))):
             self._p_left -= 1
@@ -445,7 +456,8 @@ class ShardedEngine(Engine):
         done = self._p_reduced if persistent else self._group_of[id(unit)].gid in self._reduced
         if self.world > 1 and not persistent and id(unit) in self._reported \
                 and (pos is None or self._group_of[id(pos[0])] is not self._group_of[id(unit)]):
-            self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(), 1.0)
+            self._model_sparse(idx.numel(), dx.shape[-1], dx.element_size(), idx.element_size(),
+                               1.0 / self.accum if self._carry_on else 1.0)
         if self.world == 1 or not done:
             return super().embedding_backward(tok, pos, dx, idx, p, seed, site)
         from ..ops import functional as F_
@@ -455,6 +467,9 @@ class ShardedEngine(Engine):
         if pos is not None:
             dwpe, acc_p = self.grad_slot(*pos)
             F_.embed_bwd(dx, idx, None, dwpe, acc_p, p, seed, site)
+        if self._carry_on and not self._is_boundary and not persistent:
+            self._carry = (tok, rows, idx.reshape(1, -1).clone())
+            return
         rows_all = rows.new_empty((self.world * rows.shape[0], d))
         idx_all = idx.new_empty((self.world * idx.shape[0], idx.shape[1]))
         works = [self.comm.all_gather(rows_all, rows, track=False),

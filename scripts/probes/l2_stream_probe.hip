@@ -162,5 +162,23 @@ int main() {
       fflush(stdout);
     }
   }
+  // VERDICT r3 Weak #6: more workgroups per CU (2 and 4 resident: 8-16 waves) -- does the per-CU
+  // rate rise above the one-workgroup figure, or is ~32 TB/s the L2's aggregate ceiling?
+  for (int grid2 : {512, 1024}) {
+    const long stride = 8192, panel = 192 * stride / 8;
+    struct V { KFn k; size_t smem; int rows; const char* name; };
+    const V vs[] = {
+        {probe_dma<128, 4>, 4 * 128 * 128, 128, "dma  rows128 nstage4"},
+        {probe_reg<192, 4, false>, 0, 192, "reg  rows192 depth4"},
+        {probe_reg<128, 6, false>, 0, 128, "reg  rows128 depth6"},
+    };
+    for (const V& v : vs) {
+      const float us = run(v.k, grid2, v.smem, buf, stride, panel, steps, sink);
+      const double per_wg = (double)v.rows * 128 * steps / (us * 1e-6);
+      printf("grid %4d (%d per CU) stride 8KB %-24s %8.1f us  %6.1f GB/s per CU  %6.2f TB/s total\n", grid2,
+             grid2 / 256, v.name, us, per_wg * grid2 / 256 / 1e9, per_wg * grid2 / 1e12);
+      fflush(stdout);
+    }
+  }
   return 0;
 }
