@@ -36,7 +36,7 @@
 
 // Softmax math is scalar f32: the file is built with -fno-slp-vectorize so the compiler does not
 // pack it into v_pk_* ops, which beside MFMAs cost more issue time than the two scalar ops they
-// replace (MI355X_MICROARCH 'price of one filler beside MFMAs'; measured 1-3 % slower,
+// replace (docs/MI355X_HW_NOTES.md, packed f32 VALU beside MFMAs; measured 1-3 % slower,
 // profiles/attention_ab_r2.txt).
 // DLTB_ATTN_PIPE=1: the backward kernels compute S / dP of BOTH 32-row sub-tiles of a
 // 64-row tile before the first softmax, so one sub-tile's MFMAs run under the other's VALU softmax

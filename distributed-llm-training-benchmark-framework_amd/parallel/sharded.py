@@ -200,12 +200,28 @@ class ShardedEngine(Engine):
                           bool(cfg.extra.get("carry_token_rows", os.environ.get("DLTB_CARRY_ROWS", "1") == "1")))
         self._carry = None
         # single process: the dW products of all blocks run as strided-batched GEMMs at the end of
-        # backward (parallel/wgrad.py); with shards, each group's gradient is reduce-scattered the
-        # moment it is complete, so they are issued immediately
-        self.defer_wgrad = self.world == 1 and bool(
-            cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
+        # backward (parallel/wgrad.py).  World > 1 with resident gradient buffers: the groups'
+        # buffers are one arena in forward order (equal-size block groups -> equally spaced gradient
+        # slots), a completed group waits until ``_group_batch`` groups are complete, and their dW
+        # products run as ONE strided-batched GEMM per kind before their reduce-scatters (a 1-block
+        # dW product costs 110 us per TinyGPT-A block against 58 for 4 batched,
+        # profiles/wgrad_batch_size_r2.txt); otherwise the products are issued immediately
+        batch = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
+        self._group_batch = int(cfg.extra.get("group_wgrad_batch", os.environ.get("DLTB_GROUP_WGRAD_BATCH", 4)))
+        self._arena = None
+        if self.world > 1 and self._grad_resident and batch and self._group_batch > 1:
+            self._arena = torch.empty(sum(g.total for g in self._order), dtype=dt, device=dev)
+            off = 0
+            for g in self._order:                      # forward order: block i's slots below block i+1's
+                g.grad_buf = self._arena[off:off + g.total]
+                g.grad = g.grad_buf
+                self._zero_padding(g)
+                g.grad = None
+                off += g.total
+        self.defer_wgrad = batch and (self.world == 1 or self._arena is not None)
         self._wq = WgradQueue()
-        self.wgrad_rows_reversed = self._blocks_reversed()
+        self._pend = []              # completed groups whose dW / reduce-scatter wait for a batch
+        self.wgrad_rows_reversed = self._blocks_reversed() if self.world == 1 else False
         # world 1: every group's gathered view IS its resident shard, so W^T can be cached per
         # optimizer step like the replicated engines do (NT-form dgrad GEMMs).  Measured
         # (profiles/cache_weight_t_sharded_r2.txt): TinyGPT-A ZeRO-3 (4 micro-steps per refresh)
@@ -444,6 +460,24 @@ class ShardedEngine(Engine):
             # they are handed to the owner space in _finish_backward)
         g.bwd_left -= 1
         if g.bwd_left == 0:
+            if self._arena is not None and self._wq.has(g.units):
+                self._pend.append(g)
+                if len(self._pend) >= self._group_batch:
+                    self._flush_pending()
+            elif self._arena is not None:        # nothing queued (the head, the embedding): reduce now,
+                self._flush_pending()            # after the groups completed before it
+                self._reduce_group(g)
+            else:
+                self._reduce_group(g)
+
+    def _flush_pending(self):
+        """The queued dW products of the pending groups (one strided-batched GEMM per kind), then
+        their reduce-scatters in completion order (the same on every rank)."""
+        if not self._pend:
+            return
+        self._wq.flush([u for g in self._pend for u in g.units])
+        pend, self._pend = self._pend, []
+        for g in pend:
             self._reduce_group(g)
 
     def embedding_backward(self, tok, pos, dx, idx, p, seed, site):
@@ -512,6 +546,8 @@ class ShardedEngine(Engine):
         pc = self.p_layout.owner_numel
         if pc == 0:
             return
+        if self.world > 1 and len(self._wq):
+            self._wq.flush()          # a 2-D parameter below the persistence threshold is in the queue
         self._p_reduced = True
         if self.world > 1:
             self.comm.reduce_scatter(self.rs_out[:pc], self.p_grad)
@@ -535,6 +571,7 @@ class ShardedEngine(Engine):
 
     def _finish_backward(self):
         self._wq.flush()
+        self._flush_pending()                     # (their dW products were just issued)
         self._zero_unreported()                   # slots of units that never reported: zero
         # persistent parameters: world 1 hands p_grad to the owner space here; world > 1 reduces it
         # here unless the last unit holding some already did (grads_ready)

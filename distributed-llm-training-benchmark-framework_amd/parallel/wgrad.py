@@ -62,6 +62,10 @@ class WgradQueue:
     def add(self, unit, i, dy, x, dw, accumulate):
         self._items[id(unit)].append((i, dy, x, dw, bool(accumulate)))
 
+    def has(self, units) -> bool:
+        """Whether any of ``units`` has queued products."""
+        return any(id(u) in self._items for u in units)
+
     def __len__(self):
         return sum(len(v) for v in self._items.values())
 

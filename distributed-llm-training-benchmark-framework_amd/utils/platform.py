@@ -4,7 +4,7 @@ import platform
 
 import torch
 
-# MI355X dense peaks (AMD figures with 2:1 sparsity are NOT used): MI355X_MICROARCH.md
+# MI355X dense peaks (AMD figures with 2:1 sparsity are NOT used): docs/MI355X_HW_NOTES.md
 MI355X_DENSE_BF16_FLOPS = 2.5e15
 MI355X_HBM_BYTES = 288e9
 
