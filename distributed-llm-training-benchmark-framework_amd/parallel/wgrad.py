@@ -85,6 +85,10 @@ class WgradQueue:
             DY = strided_batch([it[0] for it in items])
             X = strided_batch([it[1] for it in items])
             if DW is not None and DY is not None and X is not None:
+                if X.stride(-2) == 1 and X.stride(-1) != 1:
+                    # BLAS TN batched: hipBLASLt's heuristic solution for it faulted the GPU
+                    # (profiles/dw_layout_probe_fault_r4.txt); the layer buffers are row-major
+                    raise RuntimeError("batched dW with a column-major X operand (BLAS TN) is refused")
                 if _blt.mm(DY.transpose(1, 2), X, DW, acc):
                     pass
                 elif acc:

@@ -1,10 +1,9 @@
 #!/usr/bin/env bash
-# Round-4 GPU batch A: fault probe (chained: stops on a fault), graph-branch probe, ProcessGroupNCCL
+# Round-4 GPU batch A: graph-branch probe, ProcessGroupNCCL
 # host cost, L2 occupancy probe, emulated phases of the N-rank ZeRO-2 path.
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-bash scripts/probes/dw_layout_probe.sh || exit 1
 timeout -k 10 120 python scripts/probes/graph_branch_probe.py > gpurun_out/graph_branch.txt 2>&1 || exit 1
 tail -4 gpurun_out/graph_branch.txt
 timeout -k 10 120 python scripts/probes/pg_host_cost.py > gpurun_out/pg_host.txt 2>&1 || exit 1

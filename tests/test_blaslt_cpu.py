@@ -125,3 +125,30 @@ def test_cpp_key_matches_python():
             assert cc is None
         else:
             assert cc == [1 if py[0] == "fp16" else 0, *py[1:]]
+
+
+def test_batched_wgrad_is_never_tn():
+    """The model's batched weight gradients (layer-strided row-major buffers) are BLAS "NT"
+    (opA N, opB T); the batched "TN" form -- whose hipBLASLt heuristic solution faulted the GPU in
+    profiles/dw_layout_probe_fault_r4.txt -- is refused by the weight-gradient queue, and its key is
+    the one csrc/bindings.cpp refuses (batch > 1, opA T, opB N)."""
+    from dltb.parallel.wgrad import WgradQueue
+    L, N, dout, din = 4, 64, 48, 32
+    dy = torch.randn(L, N, dout).to(torch.bfloat16)          # layer buffers: [L, tokens, width]
+    x = torch.randn(L, N, din).to(torch.bfloat16)
+    dw = torch.zeros(L, dout, din, dtype=torch.bfloat16)
+    key = blaslt.problem(dy.transpose(1, 2), x, dw, False)
+    assert key is not None and (key[1], key[2], key[6]) == (0, 1, L)
+    # the probe's faulting form: X seen transposed from a K-contiguous [L, din, N] buffer
+    xt = x.transpose(1, 2).contiguous()
+    bad = blaslt.problem(dy.transpose(1, 2).contiguous(), xt.transpose(1, 2), dw, False)
+    assert bad is not None and (bad[1], bad[2], bad[6]) == (1, 0, L)
+    q = WgradQueue()
+
+    class U:
+        pass
+    units = [U() for _ in range(L)]
+    for i, u in enumerate(units):
+        q.add(u, 0, dy[i], xt[i].t(), dw[i], False)
+    with pytest.raises(RuntimeError, match="TN"):
+        q.flush()
