@@ -145,3 +145,34 @@ def test_bench_emulate_prediction_record():
     assert rec["config"]["parallelism"] == "zero2-dp8" and rec["world_size_seen"] == 8
     assert rec["comm_model_ms_per_step"] > 0
     assert abs(rec["wire_bytes_per_step"] - rec["wire_bytes_per_step_model"]) <= 8
+
+
+def test_world_n_wgrad_batches(monkeypatch):
+    """World > 1 keeps the weight gradients batched: ZeRO-2 plans the head as a bucket of its own and
+    the blocks in whole groups of 4 (one 4-block batched dW per kind and bucket, not 2/4/4/4/2), and
+    the sharded engines batch the dW of 4 completed block groups from their gradient arena."""
+    monkeypatch.setenv("DLTB_COMM", "emulate:8")
+    torch.manual_seed(0)
+    mcfg = get_model_config("A", 64)
+    mcfg.n_layer, mcfg.n_embd, mcfg.n_head, mcfg.vocab_size, mcfg.dropout = 8, 128, 2, 512, 0.0
+    model = build_model(mcfg)
+    blk = model.unit_blocks[0].numel
+    cfg = engine_config("zero2", 4, "reference", None, bucket_mb=4 * blk * 4 / 2**20 * 0.6)
+    eng = make_engine(model, cfg, "cpu")
+    names = [[u.name for u in b.units] for b in eng.layout.buckets]
+    assert names[0] == ["head"] and names[-1] == ["embed"], names
+    assert all(len(n) == 4 for n in names[1:-1]), names
+    for strategy in ("zero3", "fsdp"):
+        torch.manual_seed(0)
+        model = build_model(mcfg)
+        c = engine_config(strategy, 4, "uniform", None, bucket_mb=1.0)
+        c.persistence_threshold = 100             # (ZeRO-3: keep the small blocks' matrices sharded)
+        eng = make_engine(model, c, "cpu")
+        assert eng.defer_wgrad and eng._arena is not None
+        eng.train()
+        x = torch.randint(0, 512, (1, 64))
+        loss = eng(x, x)[1]
+        eng.backward(loss)
+        eng.step()
+        assert eng._wq.batched_calls == 2 * 4 and eng._wq.single_calls == 0, (strategy, eng._wq.batched_calls,
+                                                                              eng._wq.single_calls)
