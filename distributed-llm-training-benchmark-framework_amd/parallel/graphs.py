@@ -63,6 +63,10 @@ class GraphedStep:
             # reduce-scatters left in flight across micro-steps would cross graph boundaries
             engine._drain_all()
             engine._tail_defer = False
+        if getattr(engine, "_carry_on", False):
+            # token rows carried into the next micro-step would be a tensor of one graph read by the
+            # next graph, whose captured allocations may reuse its memory: exchange every micro-step
+            engine._carry_on = False
 
     def _eager(self, idx, tgt):
         loss = self.e(idx, tgt)[1]
