@@ -10,4 +10,4 @@ timeout -k 10 120 python scripts/probes/pg_host_cost.py > gpurun_out/pg_host.txt
 tail -5 gpurun_out/pg_host.txt
 timeout -k 10 120 ./scripts/probes/l2_stream_probe > gpurun_out/l2_probe.txt 2>&1 || exit 1
 tail -8 gpurun_out/l2_probe.txt
-STRAT=zero2 N=8 bash scripts/emu_phases.sh
+for S in zero2 zero3 fsdp ddp; do echo "== $S"; STRAT=$S N=8 bash scripts/emu_phases.sh || exit 1; done
