@@ -61,3 +61,16 @@ def test_world2_m7b_width_and_dropout(tmp_path):
         assert torch.equal(da["final"][n], db["final"][n]), n
     for l1, l2 in zip(d1["losses"], da["losses"]):
         assert abs(l1 - l2) < 0.02 * abs(l1), (l1, l2)
+
+
+def test_world2_deepspeed_switches_gpu(tmp_path):
+    """The DeepSpeed keys that change the communication (parallel/ds_config.py) on the bf16 HIP path:
+    overlap_comm / reduce_scatter / allgather_partitions false (synchronous collectives, all-reduce +
+    own chunk, per-owner broadcasts) and the ZeRO-3 budgets (prefetch elements, reuse-distance keep,
+    AdamW sub-groups): two host-staged ranks on the GPU train the world-1 model, eager and lazy."""
+    ex = ("--cases", "zero2_ds_switches,zero3_ds_budgets")
+    ws1 = run(tmp_path / "s1.pt", 1, "cuda", extra=ex, timeout=600)
+    for env in ({"DLTB_COMM": "host"}, {"DLTB_COMM": "host", "DLTB_COMM_LAZY": "1"}):
+        ws2 = run(tmp_path / "s2.pt", 2, "cuda", extra=ex, env_extra=env, timeout=600)
+        bad = compare(ws1, ws2, loss_tol=1e-3, upd_tol=0.02, cos_min=0.9998, param_tol=0.03)
+        assert not bad, (env, bad)
