@@ -22,14 +22,27 @@ XGMI_LINKS_PER_GPU = 7
 XGMI_LINK_GBPS = 153.0          # per direction, per link
 DEFAULT_BUS_GBPS = 300.0        # conservative RCCL bus bandwidth per rank at 8 GPUs (large messages)
 DEFAULT_ALPHA_US = 25.0         # fixed cost of one RCCL collective (launch + sync), 8 ranks
+LINK_EFFICIENCY = 0.7           # share of a link's rate a ring step sustains (assumed until measured)
 
 
-def collective_time_us(op: str, nbytes: int, world: int, bus_gbps: float = DEFAULT_BUS_GBPS,
+def default_bus_gbps(world: int) -> float:
+    """Default bus bandwidth at ``world`` ranks of one node: a rank reaches its peers over its
+    ``world - 1`` point-to-point links only, so small jobs cannot use the whole 7-link fabric (two GPUs
+    share ONE link); capped at the conservative 8-GPU figure."""
+    if world <= 1:
+        return DEFAULT_BUS_GBPS
+    return min(DEFAULT_BUS_GBPS, LINK_EFFICIENCY * XGMI_LINK_GBPS * min(world - 1, XGMI_LINKS_PER_GPU))
+
+
+def collective_time_us(op: str, nbytes: int, world: int, bus_gbps: float = None,
                        alpha_us: float = DEFAULT_ALPHA_US) -> float:
-    """alpha-beta estimate of one collective on ``nbytes`` (full buffer) at ``world`` ranks."""
+    """alpha-beta estimate of one collective on ``nbytes`` (full buffer) at ``world`` ranks
+    (default bus bandwidth: ``default_bus_gbps(world)``)."""
     from .collectives import ring_factor
     if world <= 1:
         return 0.0
+    if bus_gbps is None:
+        bus_gbps = default_bus_gbps(world)
     return alpha_us + nbytes * ring_factor(op, world) / (bus_gbps * 1e3)
 
 
@@ -88,7 +101,7 @@ def measured_params(world: int, op: str = "reduce_scatter", path: str = None):
     fit = fit_alpha_beta(rows, op, world) if rows else None
     if fit is not None:
         return fit[0], fit[1], "measured"
-    return DEFAULT_ALPHA_US, DEFAULT_BUS_GBPS, "default"
+    return DEFAULT_ALPHA_US, default_bus_gbps(world), "default"
 
 
 def calibrate_fabric(device, sizes_mb=(4, 16, 64), iters: int = 5, dtype=None, group=None,
