@@ -243,12 +243,14 @@ int dltb_blaslt_run_heuristic(const BltProblem& p, const void* A, const void* B,
       pref.setMaxWorkspaceBytes(kWorkspace);
       std::vector<hipblasLtMatmulHeuristicResult_t> r;
       if (g->algoGetHeuristic(1, pref, r) != HIPBLAS_STATUS_SUCCESS || r.empty()) return -1;
-      // solutions observed to fault the GPU on a problem they were picked for: never run them
-      // (618464: batched bf16 TN weight gradient, profiles/dw_layout_probe_fault_r4.txt)
-      static const int kDeny[] = {618464};
+      // solutions observed to fault the GPU in BATCHED form: never run them batched
+      // (618464: bf16 TN, faulted as a 16-batch 1024 x 4096 x 8192 weight gradient,
+      // profiles/dw_layout_probe_fault_r4.txt; the same solution runs the unbatched TN products --
+      // the tied head's data gradient through the cached W^T -- without fault, GPU tests r3/r4)
+      static const int kDenyBatched[] = {618464};
       const int idx = hipblaslt_ext::getIndexFromAlgo(r[0].algo);
-      for (int d : kDeny)
-        if (idx == d) return -6;
+      for (int d : kDenyBatched)
+        if (p.batch > 1 && idx == d) return -6;
       pk = picks.emplace(shape, r[0].algo).first;
     }
     auto t = tuning_of(0, 0);
