@@ -162,6 +162,7 @@ class Comm:
             # (profiles/pg_host_cost.json, scripts/probes/pg_host_cost.py); spun on the host before
             # the paced kernel is launched, so an eager emulated step pays what a real one would
             self.emu_host_us = pg_host_cost_us()
+            self.emu_null = os.environ.get("DLTB_EMU_NULL", "0") == "1"
             self.emu_params = {}          # op -> (alpha_us, bus_GBps, source)
             for op in ("all_reduce", "reduce_scatter", "all_gather", "broadcast", "all_to_all"):
                 a, b, src = measured_params(self.world, "all_reduce" if op == "all_reduce" else "reduce_scatter")
@@ -240,6 +241,10 @@ class Comm:
                     dst.view(-1)[r * rep_stride:r * rep_stride + src.numel()].copy_(v.view(-1))
             return _DONE
         from ..ops._ext import ext
+        if self.emu_null:
+            # DLTB_EMU_NULL=1 (timing only): no collective kernel and no numerics stand-in at all --
+            # the step time of the N-rank code path alone (the results are NOT the N-rank numerics)
+            return _DONE
         if self._emu_stream is None:
             self._emu_stream = torch.cuda.Stream(device=full.device, priority=-1)
             self._emu_handle = self._emu_stream.cuda_stream
@@ -274,6 +279,8 @@ class Comm:
         off = out.data_ptr() + self.rank * n * out.element_size()
         if inp.data_ptr() == off and inp.dtype == out.dtype:     # in place: the own chunk is already there
             return self._emu("all_gather", out, async_op=async_op, track=track)
+        if self.emu_null and out.is_cuda:
+            return _DONE
         if out.is_cuda and out.dtype not in (torch.bfloat16, torch.float16, torch.float32):
             # integer payloads (the embedding's token ids): replicate with a torch copy on the
             # emulation stream, the paced kernel models the transfer
