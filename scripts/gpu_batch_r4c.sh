@@ -12,3 +12,13 @@ for r in 1 2; do
     tail -n 1 gpurun_out/abtail/ddp_tail${t}_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('tail$t', $r, round(d['ms_per_step'],3))"
   done
 done
+# VERDICT r3 Weak #3: HIP-graph replay of the emulated N = 8 ZeRO-2 step vs eager (graphs drop the tail deferral and
+# the carried token rows: collectives may not stay in flight across graph boundaries)
+mkdir -p gpurun_out/abgraph
+for r in 1 2; do
+  for g in off on; do
+    timeout -k 10 200 python bench.py --strategy zero2 --emulate 8 --steps 24 --warmup 8 --graphs $g \
+        > gpurun_out/abgraph/g${g}_$r.log 2>&1 || exit 1
+    tail -n 1 gpurun_out/abgraph/g${g}_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('graphs-$g', $r, round(d['ms_per_step'],3), d.get('hip_graphs'))"
+  done
+done
