@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--hold-us", type=float, default=2000.0)
     ap.add_argument("--gemms", type=int, default=24)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--forks", type=int, default=6)
     a = ap.parse_args()
     import torch
     import dltb  # noqa: F401
@@ -61,7 +62,25 @@ def main():
         ev = paced()
         torch.cuda.current_stream().wait_event(ev)
 
-    cases = {"A_compute": compute, "B_side": join_only, "C_both": both}
+    def multi():
+        # the engines' pattern: a collective forked after each of several compute segments, all joined
+        # at the end (a reduce-scatter per gradient bucket, waited at the next micro-step)
+        evs, y = [], x
+        seg = max(1, a.gemms // a.forks)
+        for f in range(a.forks):
+            for _ in range(seg):
+                y = torch.mm(y, w)
+                y = y * 1e-2
+            side.wait_stream(torch.cuda.current_stream())
+            ext().comm_emu(None, 1, None, None, 1.0, 1, 0, float(a.hold_us) / a.forks, 0.0, 32, side.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(side)
+            evs.append(ev)
+        for ev in evs:
+            torch.cuda.current_stream().wait_event(ev)
+        return y
+
+    cases = {"A_compute": compute, "B_side": join_only, "C_both": both, "D_multi_fork": multi}
     res = {}
     for name, fn in cases.items():
         for _ in range(3):
