@@ -53,7 +53,7 @@ def build_parser():
     p.add_argument("--master-addr", type=str, default=None)
     p.add_argument("--master-port", type=int, default=None)
     # model & data
-    p.add_argument("--tier", type=str, required=True, choices=["A", "B", "default", "M7B", "tiny", "mtiny"])
+    p.add_argument("--tier", type=str, required=True, choices=["A", "B", "default", "M7B", "M7B_narrow", "tiny", "mtiny"])
     p.add_argument("--seq-len", type=int, required=True)
     p.add_argument("--synthetic", action="store_true", help="accepted for compatibility (data is always synthetic)")
     # training

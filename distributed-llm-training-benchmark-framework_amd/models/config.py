@@ -75,7 +75,7 @@ class ModelConfig:
         return 6.0 * n_mat + attn
 
 
-TIERS = ("A", "B", "default", "M7B", "tiny", "mtiny")
+TIERS = ("A", "B", "default", "M7B", "M7B_narrow", "tiny", "mtiny")
 
 
 def get_model_config(tier: str, seq_len: int, dropout: float = 0.1) -> ModelConfig:
@@ -96,6 +96,11 @@ def get_model_config(tier: str, seq_len: int, dropout: float = 0.1) -> ModelConf
     if tier == "tiny":   # unit-test shape (CPU friendly)
         return ModelConfig(vocab_size=128, n_embd=64, n_head=4, n_layer=2, block_size=seq_len,
                            dropout=dropout, tier="tiny")
+    if tier == "M7B_narrow":   # the M7B unit / collective structure (32 layers, GQA 4:1, untied head) at d 512:
+        # the host-cost proxy of an eager N-rank Mistral-7B step (scripts/m7b_host_proxy.sh)
+        return ModelConfig(arch="mistral", vocab_size=4096, n_embd=512, n_head=8, n_kv_head=2, n_layer=32,
+                           ffn_hidden=1792, block_size=seq_len, dropout=0.0, causal=True, tie_embeddings=False,
+                           rope_theta=10000.0, tier="M7B_narrow")
     if tier == "mtiny":  # Mistral-shape unit-test model: GQA 2:1, head_dim 64 (the GPU attention's smallest)
         return ModelConfig(arch="mistral", vocab_size=256, n_embd=128, n_head=2, n_kv_head=1, n_layer=2,
                            ffn_hidden=256, block_size=seq_len, dropout=0.0, causal=True,
