@@ -172,6 +172,16 @@ class ShardedEngine(Engine):
                     self._reuse_keep.add(g.gid)
                 after += g.total
         self._overlap = bool(cfg.extra.get("overlap_comm", True))
+        # ZeRO-3 / FSDP inside an accumulation window (world > 1): a micro-step that does not end its
+        # window leaves its reduce-scatters in flight instead of waiting for them at the end of its
+        # backward; the next backward's first gradient write waits for them and folds the chunks into
+        # the fp32 accumulator (one launch), a forward later, when they are long done.  The window's
+        # last micro-step drains everything before the optimizer (as the replicated engines do).
+        self._tail_defer = (self.world > 1 and self.acc is not None and self._overlap and
+                            bool(cfg.extra.get("defer_tail_reduce", True)))
+        self._rs_inflight = []       # reduce-scatter works of the current / deferred micro-step
+        self._deferred = False       # a finished micro-step's reduce-scatters are still to be drained
+        self._deferred_first = False
         if cfg.zero_stage == 3 and cfg.extra.get("reduce_bucket_elems"):
             from .ds_config import check_bucket_caps
             check_bucket_caps(cfg, [g.total for g in groups] + [p_total], "zero3")   # (+ the persistent block)
@@ -394,6 +404,8 @@ class ShardedEngine(Engine):
         return self._views(unit)
 
     def grad_slot(self, unit, i):
+        if self._deferred:
+            self._drain_all()        # the previous micro-step's reduce-scatters read these buffers
         key = (id(unit), i)
         v = self._gviews.get(key)
         if v is not None:
@@ -538,7 +550,10 @@ class ShardedEngine(Engine):
         self._reduced.add(g.gid)
         if self.world > 1:
             out = self.rs_out[g.owner_start:g.owner_start + g.chunk]
-            self.comm.reduce_scatter(out, g.grad, async_op=self._overlap)
+            if self._tail_defer:
+                self._rs_inflight.append(self.comm.reduce_scatter(out, g.grad, track=False))
+            else:
+                self.comm.reduce_scatter(out, g.grad, async_op=self._overlap)
             self._held_grads.append(g.grad)
         g.grad = None
 
@@ -549,8 +564,10 @@ class ShardedEngine(Engine):
         if self.world > 1 and len(self._wq):
             self._wq.flush()          # a 2-D parameter below the persistence threshold is in the queue
         self._p_reduced = True
-        if self.world > 1:
-            self.comm.reduce_scatter(self.rs_out[:pc], self.p_grad)
+        if self.world > 1 and self._tail_defer:
+            self._rs_inflight.append(self.comm.reduce_scatter(self.rs_out[:pc], self.p_grad, track=False))
+        elif self.world > 1:
+            self.comm.reduce_scatter(self.rs_out[:pc], self.p_grad, async_op=self._overlap)
         else:
             self.rs_out[:pc].copy_(self.p_grad)
 
@@ -583,18 +600,38 @@ class ShardedEngine(Engine):
             g.bwd_left = len(g.units)
         self._phase("comm_wait_begin")
         self._wait_works()
+        if self._tail_defer and not self._is_boundary:
+            # left in flight: drained at the next backward's first gradient write (grad_slot)
+            self._deferred, self._deferred_first = True, self._window_pos == 0
+            self._phase("comm_wait_end")
+            return
+        self._deferred, self._deferred_first = True, self._window_pos == 0
+        self._drain_all()
+        self._phase("comm_wait_end")
+
+    def _drain_all(self):
+        """Wait for the reduce-scatters of the finished micro-step, add the exchanged token rows,
+        and fold the owner chunks into the fp32 accumulator (one launch)."""
+        if not self._deferred:
+            return
+        self._deferred = False
+        for w in self._rs_inflight:
+            w.wait()
+        self._rs_inflight = []
         if self._sparse is not None:
             self._apply_sparse()
-        self._phase("comm_wait_end")
         self._held_grads.clear()
         if self.acc is not None:
-            first = self._window_pos == 0
+            first = self._deferred_first
             if self.acc.is_cuda:
                 ext().f32_from_bf16_(self.acc, self.rs_out, not first)
             elif first:
                 self.acc.copy_(self.rs_out)
             else:
                 self.acc += self.rs_out
+
+    def _wait_param_gathers(self):
+        self._drain_all()                         # (finalize / checkpoint / graph capture)
 
     def _optimizer_step(self, lr):
         g = self.acc if self.acc is not None else self.rs_out
