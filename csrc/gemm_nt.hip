@@ -28,6 +28,13 @@
 // faster than hipBLASLt (fc2 22.3 vs 25.7 us, fc1 dgrad 22.2 vs 25.5, qkv dgrad 19.4 vs 19.9;
 // profiles/gemm_nt_splitk_r3.txt), but the consuming LayerNorm would then read 16 MB of fp32 planes
 // instead of 4 MB of bf16 (~2 us more per product), which leaves ~1% of a step: not wired in.
+// Split-K with an in-kernel pair fixup (cfg 10, bf16 output, no consumer change) was built in round 4
+// to keep the split's gain without the planes: correct, but the cross-CU hand-over (store, ack, flag,
+// poll, load) adds ~6 us to a ~24 us product -- fc2 30.1 vs hipBLASLt 27.0 us, and 45 us with agent-scope
+// fences (an L2 write-back / invalidate per wave) instead of agent-coherent stores
+// (profiles/gemm_nt_pair_fixup_r4.txt): not wired in either.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 #include "mfma_tiles.h"
@@ -47,7 +54,10 @@ struct NtArgs {
   int M, N, K;
   int gm;            // m-blocks per group of the tile walk
   int accumulate;
-  float* part;       // split-K configs: fp32 partial planes part[split][M][N] (bias folded into split 0)
+  float* part;       // split-K configs: fp32 partial planes part[split][M][N] (bias folded into split 0);
+                     // pair-fixup configs: the first split's fp32 partials, wave-sub-tile-linear [M * N]
+  int* sync;         // pair-fixup configs: {arrivals, ready} per (tile, consumer wave); zero between launches
+  int fixmode;       // pair fixup: 2 = ablation without pairing (DLTB_NT_FIXMODE, timing only)
 };
 
 template <int GLDS, int N>
@@ -150,7 +160,17 @@ DLTB_DEV void nt_barrier() {
 // per-CU operand stream of the K-long products (fc2, and the fc1 / qkv data gradients), whose tile
 // grids at M = 2048, N = 1024 would otherwise hold only 128 workgroups of 128 x 128 or stream
 // 1.57 MB per CU as 256 tiles of 128 x 64.
-template <int BM, int BN, int BK, int NSTAGE, int RD, int SK = 1>
+//
+// FIX (with SK = 2): pair fixup instead of planes -- the output stays bf16 [M, N], so no consumer
+// changes.  Consumer wave w of split s of a tile pairs with wave w of the other split: the first of
+// the two to finish its k-range (an agent-scope atomic on the pair's arrival counter decides) stores
+// its fp32 accumulators to the workspace and raises the pair's ready flag (release fence first); the
+// second waits for that flag (it can only be waiting on a wave that is already running its
+// epilogue), adds the partials (acquire fence) and writes the bf16 result with the bias through the
+// ordinary epilogue, then clears the pair's counters for the next launch.  The wait is bounded: a
+// pair that never sees its flag gives up after ~2^20 polls (wrong numbers, caught by the tests,
+// instead of a wave that never retires).
+template <int BM, int BN, int BK, int NSTAGE, int RD, int SK = 1, bool FIX = false>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
   using G = NtGeo<BM, BN, BK>;
   using TA = GldsTile<BK, BM, true>;
@@ -268,7 +288,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
   for (int i = 0; i < G::FM; ++i)
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) acc[i][j] = f32x16{};
-  NtFrags<BM, BN, BK, (SK > 1)> f0, f1;
+  NtFrags<BM, BN, BK, (SK > 1 && !FIX)> f0, f1;
   nt_barrier();                  // B_init: stage 0 landed
   f0.read(smem, wm, wn, r, h);
   drain_lds_reads();
@@ -283,7 +303,58 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
     drain_lds_reads();
   }
 
-  if constexpr (SK > 1) {
+  if constexpr (SK == 2 && FIX) {
+    if (g.fixmode != 2) {   // (2: ablation without pairing -- each split writes its half; timing only)
+      const int slot = (mb * tiles_n + nb) * 4 + wv;
+      int* pair = g.sync + 2 * slot;
+      constexpr int NV = G::FM * G::FN * 8;     // 64-bit words per lane (the wave's 64 x 64 fp32 partial)
+      uint64_t* pw = reinterpret_cast<uint64_t*>(g.part) + (size_t)slot * (NV * 64) + lane;
+      int old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(pair, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old == 0) {
+        // agent-coherent stores (written through to the coherence point: no L2 write-back walk, which
+        // an agent-scope release fence costs), then the wait for their acknowledgements, then the flag
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < G::FN; ++j)
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+              const uint64_t v = (uint64_t)__float_as_uint(acc[i][j][2 * w]) |
+                                 ((uint64_t)__float_as_uint(acc[i][j][2 * w + 1]) << 32);
+              __hip_atomic_store(pw + ((i * G::FN + j) * 8 + w) * 64, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        asm volatile("" ::: "memory");
+        wait_vm<0>();
+        asm volatile("" ::: "memory");
+        if (lane == 0) __hip_atomic_store(pair + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      if (lane == 0) {
+        int polls = 0;
+        while (__hip_atomic_load(pair + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 && ++polls < (1 << 20))
+          __builtin_amdgcn_s_sleep(1);
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j)
+#pragma unroll
+          for (int w = 0; w < 8; ++w) {
+            const uint64_t v = __hip_atomic_load(pw + ((i * G::FN + j) * 8 + w) * 64, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            acc[i][j][2 * w] += __uint_as_float((uint32_t)v);
+            acc[i][j][2 * w + 1] += __uint_as_float((uint32_t)(v >> 32));
+          }
+      if (lane == 0) {
+        __hip_atomic_store(pair, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pair + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // (falls through to the bf16 epilogue: lane -> row m, as for SK = 1)
+  } else if constexpr (SK > 1) {
     // ---- split-K epilogue: lane -> column n, register e -> row (e & 3) + 8 (e >> 2) + 4 h (fp32 planes)
     float* pp = g.part + (size_t)split * g.M * g.N;
 #pragma unroll
@@ -327,28 +398,29 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel(NtArgs g) {
   }
 }
 
-template <int BM, int BN, int BK, int NSTAGE, int RD = 0, int SK = 1>
+template <int BM, int BN, int BK, int NSTAGE, int RD = 0, int SK = 1, bool FIX = false>
 void launch_nt(const NtArgs& g, hipStream_t st) {
   constexpr int smem = NSTAGE * NtGeo<BM, BN, BK>::STAGE;
   static_assert(smem <= 163840, "LDS budget");
   static_assert(RD == 0 || NSTAGE == 3, "register-staged loaders write two stages ahead into a 3-slot ring");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NSTAGE, RD, SK>,
+    (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<BM, BN, BK, NSTAGE, RD, SK, FIX>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int tiles = (g.M / BM) * (g.N / BN);
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NSTAGE, RD, SK>), dim3(tiles * SK), dim3(512), smem, st, g);
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, BK, NSTAGE, RD, SK, FIX>), dim3(tiles * SK), dim3(512), smem, st, g);
 }
 
 // tile configs: BM x BN, k-step BK, ring depth (what fits in 160 KB of LDS)
 struct NtCfg {
   int bm, bn, bk, sk;
+  bool fix = false;   // split-K with pair fixup (bf16 output) instead of fp32 planes
 };
 constexpr NtCfg kNtCfgs[] = {{128, 64, 64, 1},  {128, 128, 64, 1}, {128, 192, 32, 1}, {128, 256, 32, 1},
                              {256, 128, 32, 1}, {64, 128, 64, 1},  {128, 64, 64, 1},  {128, 128, 64, 2},
-                             {128, 64, 64, 2},  {256, 128, 32, 2}};
+                             {128, 64, 64, 2},  {256, 128, 32, 2}, {128, 128, 64, 2, true}};
 constexpr int kNtNumCfgs = sizeof(kNtCfgs) / sizeof(kNtCfgs[0]);
 
 void launch_cfg(int cfg, const NtArgs& g, hipStream_t st) {
@@ -362,7 +434,8 @@ void launch_cfg(int cfg, const NtArgs& g, hipStream_t st) {
     case 6: launch_nt<128, 64, 64, 3, 4>(g, st); break;      // register-staged loaders (A/B only)
     case 7: launch_nt<128, 128, 64, 5, 0, 2>(g, st); break;  // split-K 2 -> fp32 planes
     case 8: launch_nt<128, 64, 64, 6, 0, 2>(g, st); break;
-    default: launch_nt<256, 128, 32, 6, 0, 2>(g, st); break;
+    case 9: launch_nt<256, 128, 32, 6, 0, 2>(g, st); break;
+    default: launch_nt<128, 128, 64, 5, 0, 2, true>(g, st); break;   // split-K 2, pair fixup -> bf16
   }
 }
 
@@ -390,7 +463,14 @@ int dltb_gemm_nt_pick(int M, int N, int K) {
   return best;
 }
 
-int dltb_gemm_nt_splits(int cfg) { return cfg >= 0 && cfg < kNtNumCfgs ? kNtCfgs[cfg].sk : 1; }
+int dltb_gemm_nt_splits(int cfg) {
+  return cfg >= 0 && cfg < kNtNumCfgs && !kNtCfgs[cfg].fix ? kNtCfgs[cfg].sk : 1;
+}
+
+int dltb_gemm_nt_fixup_ints(int cfg, int M, int N) {
+  if (cfg < 0 || cfg >= kNtNumCfgs || !kNtCfgs[cfg].fix) return 0;
+  return 2 * 4 * (M / kNtCfgs[cfg].bm) * (N / kNtCfgs[cfg].bn);
+}
 
 bool dltb_gemm_nt_supported(int M, int N, int K, int cfg) {
   if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
@@ -398,10 +478,11 @@ bool dltb_gemm_nt_supported(int M, int N, int K, int cfg) {
 }
 
 int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part) {
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part, int* sync) {
   if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
   if (!dltb_gemm_nt_supported(M, N, K, cfg)) return -1;
   if (kNtCfgs[cfg].sk > 1 && (part == nullptr || accumulate)) return -1;
+  if (kNtCfgs[cfg].fix && (sync == nullptr || c == nullptr)) return -1;
   NtArgs g{};
   g.a = (const bf16_t*)a;
   g.b = (const bf16_t*)b;
@@ -416,6 +497,9 @@ int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long l
   g.gm = gm;
   g.accumulate = accumulate;
   g.part = part;
+  g.sync = sync;
+  static const int fixmode = getenv("DLTB_NT_FIXMODE") ? atoi(getenv("DLTB_NT_FIXMODE")) : 0;
+  g.fixmode = fixmode;
   launch_cfg(cfg, g, st);
   return cfg;
 }

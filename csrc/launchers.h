@@ -152,8 +152,11 @@ int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* pa
 int dltb_gemm_nt_pick(int M, int N, int K);
 bool dltb_gemm_nt_supported(int M, int N, int K, int cfg);
 int dltb_gemm_nt_splits(int cfg);   // > 1: split-K config, writes fp32 planes part[split][M][N] instead of c
+// > 0: split-K pair-fixup config (bf16 c; part = fp32 [M * N] workspace, sync = this many zeroed ints)
+int dltb_gemm_nt_fixup_ints(int cfg, int M, int N);
 int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part = nullptr);
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part = nullptr,
+                 int* sync = nullptr);
 
 // device-scalar helpers (head backward: no host sync)
 void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,

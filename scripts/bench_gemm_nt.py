@@ -21,8 +21,9 @@ from dltb.ops import blaslt  # noqa: E402
 from dltb.ops._ext import ext  # noqa: E402
 
 CFGS = {0: "128x64k64", 1: "128x128k64", 2: "128x192k32", 3: "128x256k32", 4: "256x128k32", 5: "64x128k64",
-        6: "128x64r4", 7: "128x128s2", 8: "128x64s2", 9: "256x128s2"}
+        6: "128x64r4", 7: "128x128s2", 8: "128x64s2", 9: "256x128s2", 10: "128x128s2fix"}
 SPLIT = (7, 8, 9)   # split-K configs: fp32 planes [2, M, N], summed by the consumer
+FIXUP = (10,)       # split-K with the pair fixup: bf16 output
 
 
 def products(model):
@@ -69,6 +70,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--split", action="store_true", help="also time the split-K configs (fp32 planes)")
+    ap.add_argument("--fixup", action="store_true", help="also time the split-K pair-fixup config (bf16 out)")
     a = ap.parse_args()
     C = ext()
     blaslt.load()
@@ -96,9 +98,15 @@ def main():
                          if C.gemm_nt_supported(M, N, K, c)]
         if a.split:
             variants += [(f"c{c}g{gm}", c, gm) for c in SPLIT for gm in (1, 4) if C.gemm_nt_supported(M, N, K, c)]
+        if a.fixup:
+            variants += [(f"c{c}g{gm}", c, gm) for c in FIXUP for gm in (1, 4) if C.gemm_nt_supported(M, N, K, c)]
         planes = torch.empty(2, M, N, device="cuda", dtype=torch.float32)
+        ws = torch.empty(M * N, device="cuda", dtype=torch.float32)
+        sync = torch.zeros(max(C.gemm_nt_fixup_ints(10, M, N), 1), device="cuda", dtype=torch.int32)
 
         def own(c, gm):
+            if c in FIXUP:
+                return C.gemm_nt(x, w, y_own, bias, False, c, gm, ws, sync)
             return C.gemm_nt(x, w, planes if c in SPLIT else y_own, bias, False, c, gm)
         fns = [lib] + [(lambda c=c, gm=gm: own(c, gm)) for _, c, gm in variants]
         ts = graph_time(fns, a.iters)

@@ -305,6 +305,32 @@ def test_gemm_nt_splitk(cfg, M, N, K):
     close(planes[0], ref_lo + bias.float(), 2e-3, 1e-3, "gemm_nt split-K plane 0 = first half of K + bias")
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (2048, 1024, 4096), (2048, 1024, 3072), (512, 384, 1536)])
+def test_gemm_nt_pair_fixup(M, N, K):
+    """Split-K NT GEMM with the pair fixup (cfg 10): bf16 output + bias, the two K halves summed in
+    fp32 by whichever wave of a pair finishes second; the pairs' counters are left zero, so the same
+    sync buffer serves launch after launch (3 launches here, and a fresh-buffer launch)."""
+    C_ = ext()
+    cfg = 10
+    if not C_.gemm_nt_supported(M, N, K, cfg):
+        pytest.skip("tile config does not divide this shape")
+    a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
+    a = a_full[:, 32:K + 32]
+    bias = rnd(N)
+    ref32 = a.float() @ b.float().t() + bias.float()
+    nsync = C_.gemm_nt_fixup_ints(cfg, M, N)
+    assert nsync == 8 * (M // 128) * (N // 128)
+    ws = torch.empty(M * N, device="cuda", dtype=torch.float32)
+    sync = torch.zeros(nsync, device="cuda", dtype=torch.int32)
+    for it in range(3):
+        out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        C_.gemm_nt(a, b, out, bias, False, cfg, 4, ws, sync)
+        assert bool(torch.isfinite(out).all()), "unwritten output elements"
+        close(out, ref32, 0.05, 2e-2, f"gemm_nt pair fixup (launch {it})")
+        assert int(sync.abs().sum()) == 0, "pair counters not cleared"
+    close(C_.gemm_nt(a, b, None, bias, False, cfg, 1), ref32, 0.05, 2e-2, "gemm_nt pair fixup (own buffers)")
+
+
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
