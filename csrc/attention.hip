@@ -56,6 +56,19 @@
 #ifndef DLTB_DQ_KS64
 #define DLTB_DQ_KS64 3
 #endif
+// forward ping-pong at D = 64 (KS = 2): split 1 runs its tiles half an iteration behind split 0
+// (softmax + P V of the previous tile, then S of this one), so on every SIMD one wave's MFMAs run
+// beside the other's softmax inside the same barrier interval instead of both waves doing the same
+// phase at once.  A/B: csrc/build.py --tag pp -D DLTB_FWD_PP=1 -D DLTB_FWD_KS64=2
+#ifndef DLTB_FWD_PP
+#define DLTB_FWD_PP 0
+#endif
+#ifndef DLTB_FWD_PP_NST
+#define DLTB_FWD_PP_NST 3     // ring depth under the ping-pong (4: the lagging split refills 2 stages ahead)
+#endif
+#ifndef DLTB_FWD_PP_PRIO
+#define DLTB_FWD_PP_PRIO 0    // 1: s_setprio 1 on the lagging split, 2: on the leading split
+#endif
 
 #include "attn_mask.h"
 #include "common.h"
@@ -272,7 +285,9 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
 template <int D>
 constexpr int fwd_ks() { return D == 64 ? DLTB_FWD_KS64 : 2; }   // KS = 4 (2-deep ring, 128 VGPRs) measured 2 % faster: not worth the spill risk
 template <int D, int KS>
-constexpr int fwd_nst() { return D == 64 && KS < 4 ? 3 : 2; }  // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
+constexpr int fwd_nst() {   // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
+  return D == 64 && KS == 2 && DLTB_FWD_PP ? DLTB_FWD_PP_NST : (D == 64 && KS < 4 ? 3 : 2);
+}
 template <int D>
 constexpr int fwd_stage_bytes() { return 2 * kTile * D * 2 + 1024; }   // K, V, dropout words of 4 waves
 template <int D, int KS = fwd_ks<D>()>
@@ -337,9 +352,15 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   for (int dt = 0; dt < NACC; ++dt)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) vfo[dt][hf] = tr_lane_off<D>(dt * 32, hf, lane);
+  constexpr bool PP = DLTB_FWD_PP && KS == 2 && NST >= 3;
   wait_vm<0>();        // Q fragments landed: no compiler vmcnt wait for them inside the loop
+  if (PP && spu == 1) {                          // (the lagging split refills NST - 2 stages ahead)
 #pragma unroll
-  for (int i = 0; i < NST - 1; ++i) issue(i);
+    for (int i = 0; i < NST - 2; ++i) issue(i);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i) issue(i);
+  }
 
   f32x16 oacc[NACC];
 #pragma unroll
@@ -351,100 +372,138 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   f32x16 mv = f32x16{};
   bool fresh = true;                             // wave-uniform
 
-  for (int it = 0; it < nit; ++it) {
-    const int t = it * KS + spu;                   // wave-uniform: the tile branches are scalar
-    // stage it+1 (issued only if its tile exists for this split) may stay in flight
-    static_assert(NST <= 3, "the counted wait below assumes at most one later stage in flight");
-    if (NST > 2 && it + 1 < nit && (it + 1) * KS + spu < nt) wait_vm<(NST > 2 ? GL : 0)>();
-    else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    issue(it + NST - 1);                         // refills the buffer read in iteration it - 1
-    const char* kt = stage_ptr(it);
-    const char* vt = kt + TB;
-    const uint32_t mw = DROP ? *reinterpret_cast<const uint32_t*>(kt + 2 * TB + wv * 256 + lane * 4) : 0u;
-    const int kv0 = t * kTile;
-    if (t < nt && (!CAUSAL || kv0 <= q0 + 31)) {
-      f32x16 sacc[2];
-      auto s_tile = [&]() {                        // S' = (Q c) K^T - m, the two key halves interleaved
-        const uint32_t kb = __builtin_amdgcn_readfirstlane(lds_addr(kt));
-        uint32_t ka[D / 16];
+  // one tile's work in three phases: S' = (Q c) K^T - m into sacc; softmax (row max, lazy rescale,
+  // exp2, row sums); O^T += V^T P^T with the dropout on the packed pairs
+  f32x16 sacc[2];
+  auto s_tile = [&](const char* kt, int kv0) {       // S' = (Q c) K^T - m, the two key halves interleaved
+    const uint32_t kb = __builtin_amdgcn_readfirstlane(lds_addr(kt));
+    uint32_t ka[D / 16];
 #pragma unroll
-        for (int s = 0; s < D / 16; ++s) ka[s] = lane_addr(kb, kfo[s]);
-        sacc[0] = mfma32(row_frag_at<0>(ka[0]), qf[0], mv);
-        sacc[1] = mfma32(row_frag_at<32 * D * 2>(ka[0]), qf[0], mv);
-        static_for<D / 16 - 1>([&](auto S1) {
-          constexpr int s = S1 + 1;
-          sacc[0] = mfma32(row_frag_at<0>(ka[s]), qf[s], sacc[0]);
-          sacc[1] = mfma32(row_frag_at<32 * D * 2>(ka[s]), qf[s], sacc[1]);
-        });
-        if (CAUSAL && kv0 + kTile - 1 > q0) {      // diagonal tile: mask keys > query
+    for (int s = 0; s < D / 16; ++s) ka[s] = lane_addr(kb, kfo[s]);
+    sacc[0] = mfma32(row_frag_at<0>(ka[0]), qf[0], mv);
+    sacc[1] = mfma32(row_frag_at<32 * D * 2>(ka[0]), qf[0], mv);
+    static_for<D / 16 - 1>([&](auto S1) {
+      constexpr int s = S1 + 1;
+      sacc[0] = mfma32(row_frag_at<0>(ka[s]), qf[s], sacc[0]);
+      sacc[1] = mfma32(row_frag_at<32 * D * 2>(ka[s]), qf[s], sacc[1]);
+    });
+    if (CAUSAL && kv0 + kTile - 1 > q0) {      // diagonal tile: mask keys > query
 #pragma unroll
-          for (int n = 0; n < 2; ++n)
+      for (int n = 0; n < 2; ++n)
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-              if (kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) sacc[n][i] = -INFINITY;
-        }
-      };
-      auto row_max = [&]() {                       // this tile's row max minus m
-        float mx = sacc[0][0];
+        for (int i = 0; i < 16; ++i)
+          if (kv0 + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h > qi) sacc[n][i] = -INFINITY;
+    }
+  };
+  auto row_max = [&]() {                       // this tile's row max minus m
+    float mx = sacc[0][0];
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-          for (int i = (n == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, sacc[n][i]);
-        // the other half of the row sits in lane ^ 32: one v_permlane32_swap, no LDS round trip
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-        return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      };
-      // move m by d = mx (first tile) or max(mx, 0): rescale l, O and this tile's S'.  Every
-      // visited tile holds at least one unmasked key per row (causal: kv0 <= q0), so mx is finite.
-      auto rescale = [&](float mx) {
-        const float d = fresh ? mx : fmaxf(mx, 0.f);
-        if (!fresh) {
-          const float alpha = __builtin_amdgcn_exp2f(-d);
-          l *= alpha;
+      for (int i = (n == 0 ? 1 : 0); i < 16; ++i) mx = fmaxf(mx, sacc[n][i]);
+    // the other half of the row sits in lane ^ 32: one v_permlane32_swap, no LDS round trip
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  };
+  // move m by d = mx (first tile) or max(mx, 0): rescale l, O and this tile's S'.  Every
+  // visited tile holds at least one unmasked key per row (causal: kv0 <= q0), so mx is finite.
+  auto rescale = [&](float mx) {
+    const float d = fresh ? mx : fmaxf(mx, 0.f);
+    if (!fresh) {
+      const float alpha = __builtin_amdgcn_exp2f(-d);
+      l *= alpha;
 #pragma unroll
-          for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
-        }
-        m = fresh ? mx : m + d;
+      for (int dt = 0; dt < NACC; ++dt) oacc[dt] *= alpha;
+    }
+    m = fresh ? mx : m + d;
 #pragma unroll
-        for (int n = 0; n < 2; ++n) sacc[n] -= d;
-        mv = splat16(-m);
-        fresh = false;
-      };
-      float ls0, ls1;
-      auto exps = [&]() {
-        ls0 = 0.f;
-        ls1 = 0.f;
-        static_for<32>([&](auto J) {
-          constexpr int n = J / 16, i = J % 16;
-          const float p = __builtin_amdgcn_exp2f(sacc[n][i]);
-          if constexpr (i & 1) ls1 += p;
-          else ls0 += p;
-          sacc[n][i] = p;
-        });
-      };
-      s_tile();
-      // lazy rescale: m moves only on the first tile or when a row max exceeds it by more than
-      // kRescaleLog2 (p <= 2^8 in between); wave-uniform, rare after the first tiles
-      {
-        const float mx = row_max();
-        if (fresh || __ballot(mx > kRescaleLog2)) rescale(mx);
-      }
-      exps();
-      l += ls0 + ls1;
-      const uint32_t vb = __builtin_amdgcn_readfirstlane(lds_addr(vt));
-      uint32_t va[NACC][2];
+    for (int n = 0; n < 2; ++n) sacc[n] -= d;
+    mv = splat16(-m);
+    fresh = false;
+  };
+  auto softmax = [&]() {
+    // lazy rescale: m moves only on the first tile or when a row max exceeds it by more than
+    // kRescaleLog2 (p <= 2^8 in between); wave-uniform, rare after the first tiles
+    {
+      const float mx = row_max();
+      if (fresh || __ballot(mx > kRescaleLog2)) rescale(mx);
+    }
+    float ls0 = 0.f, ls1 = 0.f;
+    static_for<32>([&](auto J) {
+      constexpr int n = J / 16, i = J % 16;
+      const float p = __builtin_amdgcn_exp2f(sacc[n][i]);
+      if constexpr (i & 1) ls1 += p;
+      else ls0 += p;
+      sacc[n][i] = p;
+    });
+    l += ls0 + ls1;
+  };
+  auto pv = [&](const char* vt, uint32_t mw) {
+    const uint32_t vb = __builtin_amdgcn_readfirstlane(lds_addr(vt));
+    uint32_t va[NACC][2];
+#pragma unroll
+    for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) va[dt][hf] = lane_addr(vb, vfo[dt][hf]);
+    static_for<4>([&](auto J) {
+      constexpr int n = J / 2, s2 = J % 2;
+      const bfx8 pf = pack_frag_keep<n, s2, DROP>(sacc[n], mw);
 #pragma unroll
       for (int dt = 0; dt < NACC; ++dt)
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) va[dt][hf] = lane_addr(vb, vfo[dt][hf]);
-      static_for<4>([&](auto J) {
-        constexpr int n = J / 2, s2 = J % 2;
-        const bfx8 pf = pack_frag_keep<n, s2, DROP>(sacc[n], mw);
-#pragma unroll
-        for (int dt = 0; dt < NACC; ++dt)
-          oacc[dt] = mfma32(tr_frag_at<(32 * n + 16 * s2) * D * 2>(va[dt][0], va[dt][1]), pf, oacc[dt]);
-      });
+        oacc[dt] = mfma32(tr_frag_at<(32 * n + 16 * s2) * D * 2>(va[dt][0], va[dt][1]), pf, oacc[dt]);
+    });
+  };
+  auto mask_word = [&](const char* st) {
+    return DROP ? *reinterpret_cast<const uint32_t*>(st + 2 * TB + wv * 256 + lane * 4) : 0u;
+  };
+  auto visible = [&](int t) { return t < nt && (!CAUSAL || t * kTile <= q0 + 31); };
+
+  if (PP && spu == 1) {
+    // ---- lagging split: [softmax + P V of tile it-1] [S of tile it] per barrier interval.  Its
+    // refill runs one stage ahead (into the slot of tile it-2, done in the previous interval),
+    // so exactly one stage is in flight at each wait.
+    constexpr int AH = NST - 2;                  // stages issued ahead
+    static_assert(!PP || AH == 1 || AH == 2, "lagging ring depth");
+    if (DLTB_FWD_PP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    bool pend = false;
+    for (int it = 0; it < nit; ++it) {
+      const int t = it * KS + spu;
+      if (AH == 2 && it + 1 < nit && (it + 1) * KS + spu < nt) wait_vm<(AH == 2 ? GL : 0)>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      issue(it + AH);
+      if (pend) {
+        const char* pst = stage_ptr(it - 1);
+        softmax();
+        pv(pst + TB, mask_word(pst));
+      }
+      pend = visible(t);
+      if (pend) s_tile(stage_ptr(it), t * kTile);
+    }
+    if (pend) {
+      const char* pst = stage_ptr(nit - 1);
+      softmax();
+      pv(pst + TB, mask_word(pst));
+    }
+  } else {
+    if (PP && DLTB_FWD_PP_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    for (int it = 0; it < nit; ++it) {
+      const int t = it * KS + spu;                   // wave-uniform: the tile branches are scalar
+      // stages it+1 .. it+NST-2 (issued only if their tiles exist for this split) may stay in flight
+      static_assert(NST <= 4, "the counted wait below assumes at most two later stages in flight");
+      const int later = NST < 3 ? 0 : min(NST - 2, min(nit - 1, (nt - 1 - spu) / KS) - it);
+      if (NST > 3 && later >= 2) wait_vm<(NST > 3 ? 2 * GL : 0)>();
+      else if (NST > 2 && later >= 1) wait_vm<(NST > 2 ? GL : 0)>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      issue(it + NST - 1);                         // refills the buffer read in iteration it - 1
+      const char* kt = stage_ptr(it);
+      if (visible(t)) {
+        const uint32_t mw = mask_word(kt);
+        s_tile(kt, t * kTile);
+        softmax();
+        pv(kt + TB, mw);
+      }
     }
   }
   __syncthreads();              // all LDS reads done before the ring is reused for the merge
