@@ -38,6 +38,10 @@ import subprocess
 import sys
 import time
 
+# multi-process GPU work on this platform needs dmabuf IPC (RCCL's peer buffers): set before any ROCm
+# runtime loads in this rank, whether the ranks came from launch() below or from an outside torchrun
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 

@@ -49,9 +49,10 @@
 #ifndef DLTB_ATTN_LPT
 #define DLTB_ATTN_LPT 1   // causal fwd / dQ grids heaviest-first (profiles/attn_lpt_order_m7b_r3.txt)
 #endif
-// key splits per workgroup at D = 64 (A/B builds: csrc/build.py --tag T -D DLTB_FWD_KS64=2)
+// key splits per workgroup at D = 64 (A/B builds: csrc/build.py --tag T -D DLTB_FWD_KS64=3); 4: 16 waves at
+// 128 VGPRs without scratch, 1.5 % faster than 3 (profiles/splitk_planes_inline_ab_r4.txt)
 #ifndef DLTB_FWD_KS64
-#define DLTB_FWD_KS64 3
+#define DLTB_FWD_KS64 4
 #endif
 #ifndef DLTB_DQ_KS64
 #define DLTB_DQ_KS64 3
@@ -283,7 +284,7 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
 }
 
 template <int D>
-constexpr int fwd_ks() { return D == 64 ? DLTB_FWD_KS64 : 2; }   // KS = 4 (2-deep ring, 128 VGPRs) measured 2 % faster: not worth the spill risk
+constexpr int fwd_ks() { return D == 64 ? DLTB_FWD_KS64 : 2; }   // KS = 4: 2-deep ring, 128 VGPRs
 template <int D, int KS>
 constexpr int fwd_nst() {   // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
   return D == 64 && KS == 2 && DLTB_FWD_PP ? DLTB_FWD_PP_NST : (D == 64 && KS < 4 ? 3 : 2);

@@ -8,13 +8,14 @@
 void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, void* s_out,
                    void* y, float* mean, float* rstd, int N, int d, float eps, bool rms,
                    uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
-                   hipStream_t st);
+                   hipStream_t st, bool r_planes = false);   // r_planes: r = fp32 split-K planes [2][N][d]
 // norm_fwd + the attention-dropout mask of (B, T, Hq) in one launch (horizontal fusion)
 void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void* b, void* s_out, void* y,
                         float* mean, float* rstd, int N, int d, float eps, bool rms, uint32_t thr16,
                         float drop_scale, const int64_t* seed, int64_t site, uint32_t* mask, int B, int T,
                         int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st,
-                        int g_begin = 0, int g_end = -1);   // tile groups [g_begin, g_end) of the mask
+                        int g_begin = 0, int g_end = -1,    // tile groups [g_begin, g_end) of the mask
+                        bool r_planes = false);
 int dltb_norm_bwd_partials(int N);
 void dltb_norm_bwd_dx(const void* dy, const void* s, const void* w, const float* mean,
                       const float* rstd, const void* dres, void* dx, int N, int d, bool rms,
@@ -32,7 +33,8 @@ int dltb_norm_bwd_fused_blocks(int N);
 bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
                          const float* rstd, const void* dres, void* dx, float* part, int N, int d,
                          bool rms, bool dxsum, hipStream_t st, void* dm = nullptr, uint32_t thr16 = 0,
-                         float drop_scale = 1.f, const int64_t* seed = nullptr, int64_t site = 0);
+                         float drop_scale = 1.f, const int64_t* seed = nullptr, int64_t site = 0,
+                         bool dy_planes = false);   // dy = fp32 split-K planes [2][N][d]
 
 // elementwise.hip
 void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st);

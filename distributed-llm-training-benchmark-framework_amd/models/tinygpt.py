@@ -146,7 +146,9 @@ class _BlockFn(torch.autograd.Function):
             x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
         f = F_.linear_fwd(h2, w1, b1)
         g = F_.gelu_fwd(f, out=lb and lb.g)
-        m = F_.linear_fwd(g, w2, b2)        # Dropout(m) + x1 happens in the consumer's LayerNorm
+        m = F_.linear_fwd_splitk(g, w2, b2) if model.splitk_planes else None
+        if m is None:
+            m = F_.linear_fwd(g, w2, b2)    # Dropout(m) + x1 happens in the consumer's LayerNorm
         rt.release_forward(unit)
         ctx.model, ctx.i, ctx.lb = model, i, lb
         ctx.fused_prev = m_in is not None   # LN1 applied the previous block's MLP dropout
@@ -188,7 +190,10 @@ class _BlockFn(torch.autograd.Function):
         dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
         df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
         wgrad(8, df, h2, ("df", "h2"))
-        dh2 = F_.linear_dgrad(df, w1, rt.weight_t(unit, 8, w1))
+        w1t = rt.weight_t(unit, 8, w1)
+        dh2 = F_.linear_dgrad_splitk(df, w1t) if model.splitk_planes else None
+        if dh2 is None:
+            dh2 = F_.linear_dgrad(df, w1, w1t)
         dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False,
                           red, bias=("dx", s[5][0], s[5][1]), dx_out=lb and lb.dx1)
         # attention
@@ -199,7 +204,10 @@ class _BlockFn(torch.autograd.Function):
                     dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:], B, T, H, H,
                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
         wgrad(2, dqkv, h1, ("dqkv", "h1"))
-        dh1 = F_.linear_dgrad(dqkv, win, rt.weight_t(unit, 2, win))
+        wint = rt.weight_t(unit, 2, win)
+        dh1 = F_.linear_dgrad_splitk(dqkv, wint) if model.splitk_planes else None
+        if dh1 is None:
+            dh1 = F_.linear_dgrad(dqkv, win, wint)
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False,
                          red, bias=(dqkv, s[3][0], s[3][1]))
         if shared is None:
@@ -290,6 +298,9 @@ class TinyGPT(nn.Module):
         # each attention-dropout mask is generated in two halves, beside the previous block's LN2
         # and beside this block's LN1 (both latency-bound row norms that leave VALU issue idle)
         self.mask_split = True         # (attribute, not an env switch: tests compare both paths)
+        # fc2 forward and the fc1 / qkv data gradients as split-K fp32 planes read by the consuming
+        # LayerNorm kernels (ops/functional.py linear_fwd_splitk); A/B switch, default off
+        self.splitk_planes = os.environ.get("DLTB_SPLITK_PLANES", "0") == "1"
         self._next_amask = None
         self._build_units()
 

@@ -594,3 +594,36 @@ def test_attn_mask_words_match_reference():
     cols = torch.arange(T, dtype=torch.int64, device=DEV)[None, :]
     want = rng.keep_mask(s, rows, cols, p).view(B * H, T, T)
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("N,d", [(512, 1024), (256, 768)])
+def test_norms_read_splitk_planes(N, d):
+    """The norm kernels' split-K inputs: a residual r (forward, with its dropout) or an upstream
+    gradient dy (fused backward) given as two fp32 planes [2, N, d] give what the same kernels give
+    for the planes' sum (rounded to bf16 there, so within bf16 tolerance)."""
+    from dltb.ops import functional as F_
+    C = ext()
+    x, w, b = rnd(N, d), rnd(d, scale=0.5) + 1, rnd(d, scale=0.1)
+    planes = torch.randn(2, N, d, device=DEV)
+    flat = planes.sum(0).to(torch.bfloat16)
+    sd = seed_obj(5)
+    s_p, y_p, mean_p, rstd_p = C.norm_fwd(x, planes, w, b, 1e-5, False, 0.1, sd.device_tensor, 9)
+    s_f, y_f, mean_f, rstd_f = C.norm_fwd(x, flat, w, b, 1e-5, False, 0.1, sd.device_tensor, 9)
+    close(s_p, s_f, 2e-2, 2e-2, "residual stream from planes")
+    close(y_p, y_f, 3e-2, 3e-2, "LN output from planes")
+    # fused backward: dy as planes vs dy as their bf16 sum
+    s_, dres = rnd(N, d), rnd(N, d)
+    mean = torch.randn(N, device=DEV) * 0.1
+    rstd = torch.rand(N, device=DEV) + 0.5
+    outs = []
+    for dy in (planes, flat):
+        gw = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
+        gb = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
+        bs = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
+        red = F_.GradReducer()
+        dx = F_.norm_bwd(dy, s_, w, mean, rstd, dres, gw, gb, False, False, red=red, bias=("dx", bs, False))
+        red.flush()
+        outs.append((dx, gw, gb, bs))
+    for a, b_, what in zip(outs[0], outs[1], ("dx", "dgamma", "dbeta", "dx column sum")):
+        assert bool(torch.isfinite(a.float()).all()), what
+        close(a, b_, 5e-2 if what == "dx" else 0.5, 3e-2, f"{what} from planes")
