@@ -28,3 +28,15 @@ def test_rccl_equivalence_script_cpu(tmp_path):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     v = json.loads(out.read_text())
     assert v["pass"] and v["world_sizes"]["2"]["mismatches"] == [] and len(v["world_sizes"]["2"]["cases"]) == 8
+
+
+def test_world8_equals_world1_cpu(tmp_path):
+    """The driver's largest world size: 8 gloo ranks (every rank's layout, owner chunks, bucket
+    partition and all-gather sizes at N = 8, real collectives) against one rank on the concatenated
+    8-row batch, every engine, at the world-2 test's bounds."""
+    extra = ("--ref-batch", "8")
+    ws1 = run(tmp_path / "ws1.pt", 1, "cpu", extra=extra)
+    ws8 = run(tmp_path / "ws8.pt", 8, "cpu", extra=extra)
+    assert set(ws1) == set(ws8)
+    bad = compare(ws1, ws8, loss_tol=1e-4, upd_tol=1e-3, cos_min=0.99999, param_tol=1e-3)
+    assert not bad, bad

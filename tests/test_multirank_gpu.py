@@ -39,6 +39,24 @@ def test_world2_host_staged_equals_world1_gpu(tmp_path):
     assert not bad, bad
 
 
+def test_world8_host_staged_equals_world1_gpu(tmp_path):
+    """The driver's largest world size on one MI355X: 8 ranks share cuda:0 through host-staged gloo
+    (every rank's N = 8 layout, owner chunks, bucket partition, all-gather sizes and bf16 HIP kernels),
+    against one rank on the concatenated 8-row batch; then the same with every collective lazy
+    (DLTB_COMM_LAZY=1, a misplaced wait changes the result).  World-2 bounds."""
+    extra = ("--ref-batch", "8")
+    ws1 = run(tmp_path / "ws1.pt", 1, "cuda", extra=extra, timeout=600)
+    ws8 = run(tmp_path / "ws8.pt", 8, "cuda", extra=extra, env_extra={"DLTB_COMM": "host"}, timeout=900)
+    assert set(ws1) == set(ws8)
+    print("[multirank] host-staged ws8 vs ws1:", json.dumps(report(ws1, ws8)))
+    bad = compare(ws1, ws8, loss_tol=1e-3, upd_tol=0.02, cos_min=0.9998, param_tol=0.03)
+    assert not bad, bad
+    ws8l = run(tmp_path / "ws8l.pt", 8, "cuda", extra=extra + ("--cases", "zero2,zero3,fsdp"),
+               env_extra={"DLTB_COMM": "host", "DLTB_COMM_LAZY": "1"}, timeout=900)
+    bad = compare({k: ws1[k] for k in ws8l}, ws8l, loss_tol=1e-3, upd_tol=0.02, cos_min=0.9998, param_tol=0.03)
+    assert not bad, bad
+
+
 def test_world2_m7b_width_and_dropout(tmp_path):
     """BASELINE config #5's layer shapes at full width (d4096, GQA 32/8, SwiGLU 14336; 2 layers)
     under ZeRO-3 at world 2 == world 1; and dropout streams: distinct per rank, deterministic,
