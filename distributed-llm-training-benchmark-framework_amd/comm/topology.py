@@ -197,9 +197,18 @@ def recommend_bucket_mb(world: int, overhead: float = 0.2, bus_gbps: float = Non
     f = ring_factor(op, world)
     need = alpha_us / overhead * bus_gbps * 1e3 / f       # bytes
     mb = 1.0
-    while mb * (1 << 20) < need and mb < 1024:
+    while mb * (1 << 20) < need and mb < BUCKET_MB_MAX:
         mb *= 2
-    return mb
+    return min(mb, BUCKET_MB_MAX)
+
+
+# Upper bound of the recommendation.  The replicated engines round a bucket up to whole groups of 4
+# transformer blocks (the batched-dW size, parallel/replicated.py), so every value up to one such
+# group (101 MB at TinyGPT-A) gives the same 4-block buckets that the emulated predictions were
+# measured with, while a larger one doubles the group and halves the number of collectives that can
+# overlap the backward.  An in-job 3-point fit (calibrate_fabric) with an inflated intercept -- a
+# first-call or protocol-switch cost at the 4 MiB point -- must not push a job there.
+BUCKET_MB_MAX = 64.0
 
 
 def parse_topology(text: str):

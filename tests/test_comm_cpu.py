@@ -167,3 +167,6 @@ def test_calibrated_params_take_precedence(tmp_path, monkeypatch):
     assert tp.measured_params(8) == (12.0, 400.0, "calibrated")
     # 12 us at 400 GB/s: need 12/0.2 us * 400 GB/s / (7/8) = 27 MB -> 32 MiB
     assert tp.recommend_bucket_mb(8) == 32.0
+    # an inflated in-job intercept (500 us: would need 171 MB) stays at the validated 4-block bucket size
+    monkeypatch.setitem(tp._CALIBRATED, (8, "reduce_scatter"), (500.0, 300.0))
+    assert tp.recommend_bucket_mb(8) == tp.BUCKET_MB_MAX == 64.0
