@@ -7,6 +7,10 @@ dropout-backward paths were measured neutral or slower and deleted):
 * DLTB_DEFER_OPT                  -- world > 1 only: tests/test_multirank_gpu.py runs ZeRO-1/2 both ways
 * DLTB_DKDV_GSPLIT                -- causal GQA dK/dV head split, forced off vs auto, below
 * DLTB_COMM_HIGH_PRIORITY         -- an RCCL stream priority (no effect on results; needs >1 GPU)
+* DLTB_SPLITK_PLANES              -- split-K fp32 planes read by the norms (round 4, off: slower in the step);
+                                     tests/test_model_gpu.py::test_splitk_planes_step_matches_hipblaslt_step
+* DLTB_FWD_PP / DLTB_NT_FIXMODE   -- build-time / A-B-only kernel variants (attention ping-pong, split-K pair
+                                     fixup ablation); their numerics run in tests/test_kernels_gpu.py on A/B builds
 """
 import os
 import subprocess
