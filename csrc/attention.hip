@@ -581,8 +581,12 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(AttnArgs P) {
 // partial dK/dV accumulators merge through LDS at the end.  Dropout folds into
 //   pd = p & keep,  ds' = p * ((dp & keep) - delta / s)     (s = 1/(1-p); dK, dV scaled by s at the store)
 // so each probability costs bfe + 2 and + sub + mul besides its exp.
+#ifndef DLTB_DKDV_KS64
+#define DLTB_DKDV_KS64 2   // query splits per dK/dV workgroup at D = 64; 3 (168 VGPRs, 80 B scratch) is 25 % slower
+                           // (profiles/attention_dkdv_ks3_ab_r4.txt)
+#endif
 template <int D>
-constexpr int dkdv_ks() { return D == 64 ? 2 : 1; }
+constexpr int dkdv_ks() { return D == 64 ? DLTB_DKDV_KS64 : 1; }
 // dropout words in LDS: [4 subs][kTile rows] with a 4-word pad per sub, so the two subs a wave
 // reads together (lanes with key bit 2 clear / set) and the 4 subs one store instruction writes
 // start 68 words apart -- different banks, where an unpadded 64-word stride put them all on the
