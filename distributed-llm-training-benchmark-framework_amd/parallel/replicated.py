@@ -454,11 +454,26 @@ class ReplicatedEngine(Engine):
         if not self._use_ag:
             self._regather(async_op=False)
             return
-        for b in reversed(range(len(self.layout.buckets))):     # forward order: embedding first
+        for b in self._gather_order():
             bk = self.layout.buckets[b]
             full = self.flat_param[bk.start:bk.end]
             mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
             self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
+
+    def _gather_order(self):
+        """Bucket order of the deferred parameter all-gathers: forward order, except that the bucket of
+        the tied token table (the head unit's parameter, which the embedding reads first of all) leads.
+        In plain forward order it came last, and the all-gathers run in issue order on one stream, so
+        the embedding's forward waited for every bucket's all-gather of the window."""
+        order = list(reversed(range(len(self.layout.buckets))))
+        tu = getattr(self.model, "tok_slot", (None,))[0]
+        bt = self._bucket_of.get(id(tu)) if tu is not None else None
+        if os.environ.get("DLTB_AG_TIED_FIRST", "1") != "1":     # (A/B: the old plain forward order)
+            bt = None
+        if bt is not None and bt in order:
+            order.remove(bt)
+            order.insert(0, bt)
+        return order
 
     def _regather(self, async_op=True):
         """Re-replicate the updated parameter chunks: an all-gather per bucket, or (DeepSpeed's
