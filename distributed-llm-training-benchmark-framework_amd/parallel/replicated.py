@@ -34,6 +34,10 @@ import os
 
 import torch
 
+
+def g_is_cuda(t):
+    return t is not None and t.is_cuda
+
 from ..ops import functional as F_
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
@@ -450,15 +454,33 @@ class ReplicatedEngine(Engine):
         self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
 
     def _deferred_optimizer_step(self, lr):
+        pipelined = (self._use_ag and self.scaler is None and g_is_cuda(self._owner_grad()) and
+                     not self.opt.sub_group and os.environ.get("DLTB_OPT_PIPELINE", "1") == "1")
+        if pipelined:
+            # clip coefficient once, then per bucket (gather order): its AdamW rows, then its
+            # all-gather -- the all-gather of the tied table's bucket starts after that bucket's
+            # update instead of after the whole shard's, and every later one earlier by the rest
+            g = self._owner_grad()
+            gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), True)
+            self.opt.prepare(lr)
+            seg = {b: i for i, b in enumerate(i for i, bk in enumerate(self.layout.buckets) if bk.chunk > 0)}
+            for b in self._gather_order():
+                if b in seg:
+                    self.opt.launch_segment(seg[b], g, gscale)
+                self._issue_gather(b)
+            return
         self._update(lr)
         if not self._use_ag:
             self._regather(async_op=False)
             return
         for b in self._gather_order():
-            bk = self.layout.buckets[b]
-            full = self.flat_param[bk.start:bk.end]
-            mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
-            self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
+            self._issue_gather(b)
+
+    def _issue_gather(self, b):
+        bk = self.layout.buckets[b]
+        full = self.flat_param[bk.start:bk.end]
+        mine = full[self.rank * bk.chunk:(self.rank + 1) * bk.chunk]
+        self._ag_pending[b] = self.comm.all_gather(full, mine, track=False)
 
     def _gather_order(self):
         """Bucket order of the deferred parameter all-gathers: forward order, except that the bucket of
