@@ -164,6 +164,9 @@ class ShardedEngine(Engine):
         # forward and backward) stay within stage3_max_reuse_distance and the gathered total within
         # stage3_max_live_parameters (DeepSpeed's release rule), instead of released and re-gathered
         self._prefetch_elems = int(cfg.extra.get("prefetch_elems", 0)) if cfg.zero_stage == 3 else 0
+        tu = getattr(self.model, "tok_slot", (None,))[0]
+        self._tied_group = self._group_of.get(id(tu)) if (tu is not None and self.world > 1 and
+                                                          os.environ.get("DLTB_AG_TIED_FIRST", "1") == "1") else None
         self._reuse_keep = set()
         if cfg.zero_stage == 3 and not self.keep_all and cfg.max_reuse_distance:
             after = 0
@@ -377,6 +380,12 @@ class ShardedEngine(Engine):
     # ------------------------------------------------------------------ runtime interface
     def acquire(self, unit):
         g = self._group_of[id(unit)]
+        tg = self._tied_group
+        if tg is not None and tg.full is None and tg is not g:
+            # the tied token table (the head unit's parameter) is read by the embedding, the first
+            # forward op: its gather goes out ahead of the embedding's own and of the prefetched
+            # blocks, which it would otherwise queue behind on the collective stream
+            self._launch_gather(tg)
         self._ensure(g)
         if self.cfg.extra.get("forward_prefetch", True):
             self._prefetch(g, +1)
