@@ -34,10 +34,6 @@ import os
 
 import torch
 
-
-def g_is_cuda(t):
-    return t is not None and t.is_cuda
-
 from ..ops import functional as F_
 from ..ops._ext import ext
 from ..optim.adamw import FlatAdamW
@@ -454,13 +450,12 @@ class ReplicatedEngine(Engine):
         self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
 
     def _deferred_optimizer_step(self, lr):
-        pipelined = (self._use_ag and self.scaler is None and g_is_cuda(self._owner_grad()) and
-                     not self.opt.sub_group and os.environ.get("DLTB_OPT_PIPELINE", "1") == "1")
-        if pipelined:
+        g = self._owner_grad()
+        if (self._use_ag and self.scaler is None and g.is_cuda and not self.opt.sub_group
+                and os.environ.get("DLTB_OPT_PIPELINE", "1") == "1"):
             # clip coefficient once, then per bucket (gather order): its AdamW rows, then its
             # all-gather -- the all-gather of the tied table's bucket starts after that bucket's
             # update instead of after the whole shard's, and every later one earlier by the rest
-            g = self._owner_grad()
             gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), True)
             self.opt.prepare(lr)
             seg = {b: i for i, b in enumerate(i for i, bk in enumerate(self.layout.buckets) if bk.chunk > 0)}
