@@ -69,7 +69,8 @@ class FlatLayout:
 
 def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 0,
                 align: int = ALIGN, shard: bool = False, param_filter=None,
-                solo_tail: int = 0, bucket_max: int = 0, solo_head: int = 0) -> FlatLayout:
+                solo_tail: int = 0, bucket_max: int = 0, solo_head: int = 0,
+                early_elems: int = 0, early_count: int = 0) -> FlatLayout:
     """Lay ``units`` (already in the desired memory order) out in one flat buffer.
 
     ``bucket_elems``: close a bucket once it holds at least this many elements (0 = one bucket per
@@ -82,6 +83,10 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
     ``solo_head``: the first ``solo_head`` units get a bucket each (in backward order the LM head:
     its collective starts right after the first backward op, and the repeated blocks behind it then
     fill their buckets in whole groups).
+    ``early_elems`` / ``early_count``: the first ``early_count`` buckets after the solo head ones close at
+    ``early_elems`` instead of ``bucket_elems`` (larger buckets early in the backward -- fewer collectives
+    while there is compute to hide them -- and the usual size at its end, which is the start of the
+    next forward's parameter all-gathers).
     ``bucket_max``: a hard upper bound (DeepSpeed's ``reduce_bucket_size`` / ``allgather_bucket_size``
     semantics): a unit that would push the open bucket past it starts a new bucket.  Units are never
     split, so a unit larger than the bound forms a bucket of its own.
@@ -100,6 +105,12 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
         return b.end
 
     tail_from = len(units) - max(0, int(solo_tail))
+    if early_count > 0 and early_elems > 0:
+        # an early bucket only where at least one usual-size bucket of the repeated units stays behind
+        # it (the last bucket of the backward, the first all-gather of the next forward)
+        regular = sum(u.numel for ui, u in enumerate(units) if max(0, int(solo_head)) <= ui < tail_from)
+        if regular < early_count * early_elems + bucket_elems:
+            early_count = 0
     def unit_end(u, start):
         """End offset of ``u``'s parameters if placed from ``start`` (same rules as below)."""
         e = start
@@ -135,7 +146,11 @@ def plan_layout(units: Sequence[Unit], world_size: int = 1, bucket_elems: int = 
         if placed:
             cur.units.append(u)
             unit_bucket[id(u)] = cur.index
-            if bucket_elems <= 0 or cur.end - cur.start >= bucket_elems or ui >= tail_from or ui < solo_head:
+            # buckets already closed after the solo head ones (the current one is the last in the list)
+            n_early = len(buckets) - 1 - min(len(buckets) - 1, max(0, int(solo_head)))
+            limit = early_elems if (early_count > 0 and early_elems > 0 and n_early < early_count
+                                    and ui >= solo_head) else bucket_elems
+            if bucket_elems <= 0 or cur.end - cur.start >= limit or ui >= tail_from or ui < solo_head:
                 off = close(cur)
                 cur = None
     if cur is not None:

@@ -83,11 +83,18 @@ class ReplicatedEngine(Engine):
             # shares the first bucket with two blocks and the blocks' dW batches come out 2/4/4/4/2
             # (a 2-block batch costs 75 us per block against 58 for 4, profiles/wgrad_batch_size_r2.txt)
             solo_head = int(cfg.extra.get("solo_head_units", os.environ.get("DLTB_SOLO_HEAD", 1)))
+        # the first bucket(s) after the head: twice the size (fewer collectives early in the backward,
+        # while compute hides them; the buckets at its end -- the first parameter all-gathers of the
+        # next forward -- keep the usual size): emulated ZeRO-2 N = 8 -0.7 %, N = 2 -0.5 %
+        # (profiles/emulated_ab_early_bucket_r4.txt).  DLTB_EARLY_BUCKETS (count; 0 = off).
+        early = int(cfg.extra.get("early_buckets", os.environ.get("DLTB_EARLY_BUCKETS", 1))) \
+            if (self.world > 1 and bucket_elems > 0) else 0
         shard = self.stage >= 1
         self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
                                       solo_tail=int(cfg.extra.get("solo_tail_units",
                                                                   os.environ.get("DLTB_SOLO_TAIL", solo_tail))),
-                                      bucket_max=ds_cap, solo_head=solo_head)
+                                      bucket_max=ds_cap, solo_head=solo_head,
+                                      early_elems=2 * bucket_elems if early else 0, early_count=early)
         # DeepSpeed switches (zero2.json; all true there and by default): overlap_comm false waits
         # for every collective where it is issued; reduce_scatter false all-reduces each bucket and
         # keeps this rank's chunk; allgather_partitions false re-replicates the updated parameters

@@ -55,6 +55,9 @@ EXTRA_CASES = {
     # last units (not all: reuse distance below the model size) and AdamW sub-groups
     "zero3_ds_budgets": dict(strategy="zero3", extra={"prefetch_elems": 1_700_000, "sub_group_elems": 300_000},
                              over={"max_live_parameters": 10**9, "max_reuse_distance": 2_200_000}),
+    # 12 blocks: the replicated engines' bucket plan head | 8 blocks (the early bucket) | 4 blocks | embedding,
+    # with the tied table's all-gather first and the per-bucket AdamW + all-gather pipeline
+    "zero2_deep": dict(strategy="zero2", layers=12),
 }
 
 
@@ -76,6 +79,8 @@ def run_case(name, spec, world, rank, device, a):
     from dltb.parallel import engine_config, make_engine
     torch.manual_seed(0)
     mcfg = model_config(spec.get("tier", "A"), a.seq_len, spec.get("dropout", 0.0))
+    if "layers" in spec:
+        mcfg.n_layer = int(spec["layers"])
     with torch.device(device):
         model = build_model(mcfg)
     init = {n: p.detach().float().cpu().clone() for n, p in model.named_parameters()}

@@ -162,6 +162,13 @@ def test_world_n_wgrad_batches(monkeypatch):
     names = [[u.name for u in b.units] for b in eng.layout.buckets]
     assert names[0] == ["head"] and names[-1] == ["embed"], names
     assert all(len(n) == 4 for n in names[1:-1]), names
+    # 16 blocks: the first bucket after the head takes 8 (fewer collectives early in the backward), the
+    # last ones keep 4 (the next forward's first parameter all-gathers)
+    mcfg16 = get_model_config("A", 64)
+    mcfg16.n_layer, mcfg16.n_embd, mcfg16.n_head, mcfg16.vocab_size, mcfg16.dropout = 16, 128, 2, 512, 0.0
+    eng16 = make_engine(build_model(mcfg16), engine_config("zero2", 4, "reference", None,
+                                                           bucket_mb=4 * blk * 4 / 2**20 * 0.6), "cpu")
+    assert [len(b.units) for b in eng16.layout.buckets] == [1, 8, 4, 4, 1]
     for strategy in ("zero3", "fsdp"):
         torch.manual_seed(0)
         model = build_model(mcfg)

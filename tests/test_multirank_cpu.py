@@ -40,3 +40,14 @@ def test_world8_equals_world1_cpu(tmp_path):
     assert set(ws1) == set(ws8)
     bad = compare(ws1, ws8, loss_tol=1e-4, upd_tol=1e-3, cos_min=0.99999, param_tol=1e-3)
     assert not bad, bad
+
+
+def test_world_n_early_bucket_plan_cpu(tmp_path):
+    """A 12-block model under ZeRO-2 at world 2 and 8 (bucket plan head | 8 | 4 | embedding, the early
+    bucket of parallel/replicated.py) against one rank on the concatenated batch."""
+    extra = ("--ref-batch", "8", "--cases", "zero2_deep")
+    ws1 = run(tmp_path / "ws1.pt", 1, "cpu", extra=extra)
+    for w in (2, 8):
+        got = run(tmp_path / f"ws{w}.pt", w, "cpu", extra=extra)
+        bad = compare(ws1, got, loss_tol=1e-4, upd_tol=1e-3, cos_min=0.99999, param_tol=1e-3)
+        assert not bad, (w, bad)

@@ -55,6 +55,13 @@ def test_world8_host_staged_equals_world1_gpu(tmp_path):
                env_extra={"DLTB_COMM": "host", "DLTB_COMM_LAZY": "1"}, timeout=900)
     bad = compare({k: ws1[k] for k in ws8l}, ws8l, loss_tol=1e-3, upd_tol=0.02, cos_min=0.9998, param_tol=0.03)
     assert not bad, bad
+    # 12 blocks under ZeRO-2 (bucket plan head | 8 | 4 | embedding: the early bucket), lazy collectives
+    deep = extra + ("--cases", "zero2_deep")
+    d1 = run(tmp_path / "d1.pt", 1, "cuda", extra=deep, timeout=600)
+    d8 = run(tmp_path / "d8.pt", 8, "cuda", extra=deep, env_extra={"DLTB_COMM": "host", "DLTB_COMM_LAZY": "1"},
+             timeout=900)
+    bad = compare(d1, d8, loss_tol=1e-3, upd_tol=0.02, cos_min=0.9998, param_tol=0.03)
+    assert not bad, bad
 
 
 def test_world2_m7b_width_and_dropout(tmp_path):
