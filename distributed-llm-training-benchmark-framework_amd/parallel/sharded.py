@@ -381,10 +381,10 @@ class ShardedEngine(Engine):
     def acquire(self, unit):
         g = self._group_of[id(unit)]
         tg = self._tied_group
-        if tg is not None and tg.full is None and tg is not g:
+        if tg is not None and tg.full is None and tg is not g and self._pos[g.gid] == 0:
             # the tied token table (the head unit's parameter) is read by the embedding, the first
-            # forward op: its gather goes out ahead of the embedding's own and of the prefetched
-            # blocks, which it would otherwise queue behind on the collective stream
+            # forward op: at the first unit's acquire its gather goes out ahead of the embedding's own
+            # and of the prefetched blocks, which it would otherwise queue behind on the collective stream
             self._launch_gather(tg)
         self._ensure(g)
         if self.cfg.extra.get("forward_prefetch", True):
