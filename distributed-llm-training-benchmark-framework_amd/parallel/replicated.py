@@ -87,8 +87,11 @@ class ReplicatedEngine(Engine):
         # while compute hides them; the buckets at its end -- the first parameter all-gathers of the
         # next forward -- keep the usual size): emulated ZeRO-2 N = 8 -0.7 %, N = 2 -0.5 %
         # (profiles/emulated_ab_early_bucket_r4.txt).  DLTB_EARLY_BUCKETS (count; 0 = off).
+        # (ZeRO-2 only: DDP and ZeRO-1 wait for every bucket before the optimizer of the same
+        # micro-step / window, and there a later first collective only lengthens the exposed tail --
+        # DDP fp16 with fp32 all-reduce N = 8 63.6 -> 60.3 %, profiles/emulated_ab_early_bucket_r4.txt)
         early = int(cfg.extra.get("early_buckets", os.environ.get("DLTB_EARLY_BUCKETS", 1))) \
-            if (self.world > 1 and bucket_elems > 0) else 0
+            if (self.world > 1 and bucket_elems > 0 and self.stage == 2) else 0
         shard = self.stage >= 1
         self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
                                       solo_tail=int(cfg.extra.get("solo_tail_units",
