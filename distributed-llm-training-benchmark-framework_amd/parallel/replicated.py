@@ -97,7 +97,8 @@ class ReplicatedEngine(Engine):
                                       solo_tail=int(cfg.extra.get("solo_tail_units",
                                                                   os.environ.get("DLTB_SOLO_TAIL", solo_tail))),
                                       bucket_max=ds_cap, solo_head=solo_head,
-                                      early_elems=2 * bucket_elems if early else 0, early_count=early)
+                                      early_elems=int(os.environ.get("DLTB_EARLY_MULT", 2)) * bucket_elems
+                                      if early else 0, early_count=early)
         # DeepSpeed switches (zero2.json; all true there and by default): overlap_comm false waits
         # for every collective where it is issued; reduce_scatter false all-reduces each bucket and
         # keeps this rank's chunk; allgather_partitions false re-replicates the updated parameters
