@@ -110,6 +110,44 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+# shipped emulated-fabric predictions (scripts/emulated_scaling.py), newest first: a real N-GPU run reports
+# the prediction for its own (strategy label, dtype, N) so the prediction error reads off one JSON line
+PREDICTION_TABLES = ["profiles/emulated_scaling_r5.jsonl", "profiles/emulated_scaling_r4_final.jsonl",
+                     "profiles/emulated_scaling_r4.jsonl"]
+
+
+def predicted_row(parallelism: str, dtype: str, world: int):
+    """The shipped prediction for this configuration, or None: {ms_per_step, value, table}."""
+    for rel in PREDICTION_TABLES:
+        path = os.path.join(ROOT, rel)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            for line in f:
+                try:
+                    d = json.loads(line)
+                except ValueError:
+                    continue
+                if (d.get("prediction") and d.get("emulated_world") == world and d.get("dtype") == dtype
+                        and d.get("config", {}).get("parallelism") == parallelism):
+                    return {"ms_per_step": d.get("ms_per_step"), "value": d.get("value"), "table": rel}
+    return None
+
+
+def comm_environment():
+    """The RCCL build and the communication knobs in effect in this rank (for a real N > 1 run)."""
+    import torch
+    ver = None
+    try:
+        v = torch.cuda.nccl.version()
+        ver = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 - gloo / CPU runs have no RCCL
+        pass
+    knobs = {k: v for k, v in sorted(os.environ.items())
+             if k.startswith(("NCCL_", "RCCL_", "HSA_", "TORCH_NCCL_", "HIP_", "GPU_MAX_HW_QUEUES"))}
+    return {"rccl_version": ver, "hip_version": getattr(torch.version, "hip", None), "knobs": knobs}
+
+
 def launch(args, argv) -> int:
     """Launcher mode: N ranks under torch.distributed.run as a child process.  Nothing here
     initialises the GPU (no torch import at all), so the parent never holds a device context."""
@@ -322,6 +360,15 @@ def run_rank(args) -> int:
                                         "bucket_mb_from": "calibrated" if args.bucket_mb is None else "flag"}
                                        if fabric else None),
             }
+            if world > 1 and not args.emulate:
+                # a real multi-rank run explains itself: RCCL build and knobs, the in-job fabric fit
+                # (fabric_calibration), the measured phase split (phase_ms, eager ranks) and the
+                # shipped prediction for exactly this configuration
+                pred = predicted_row(f"{label}-dp{world}", out["dtype"], world)
+                out["comm_env"] = comm_environment()
+                out["predicted"] = pred
+                out["prediction_error"] = ((ms - pred["ms_per_step"]) / pred["ms_per_step"]
+                                           if pred and pred.get("ms_per_step") else None)
             if args.emulate:
                 out.update({
                     "metric": "tokens_per_sec_predicted",

@@ -1,0 +1,337 @@
+// bf16 "NT" GEMM with register-staged operands for the per-layer products of a training step
+// (gfx950, CDNA4):
+//
+//   C[M, N] = A[M][K] . B[N][K]^T  (+ bias[n])  (+ C when accumulating)       fp32 accumulate
+//
+// Every forward product (x W^T) and every data gradient against the cached W^T of a TinyGPT /
+// Mistral block has this form with M = tokens.  At M = 2048 the output of one product is only
+// 2-8 M elements, so one tile per CU is all the parallelism there is; each CU then has to pull
+// (BM + BN) x K x 2 bytes of operands through its 64 B/clk L2 -> CU path, and that stream -- not
+// the MFMAs -- sets the floor of the N = 1024 products (docs: profiles/gemm_roofline_r5.txt).
+//
+// Design (round 5, replaces gemm_nt.hip's LDS-DMA loader/consumer split as the step's kernel):
+//   * 256 threads = 4 waves, one workgroup per CU; every wave both loads and multiplies.
+//   * Operands are staged global -> VGPRs -> LDS.  A plain global_load_dwordx4 costs its wave a
+//     few issue cycles (an LDS-DMA instruction holds its wave ~60-100), so the loads of D stages
+//     can be kept in flight in registers between the MFMAs of the current stage: per thread and
+//     stage NA + NB 16-byte pieces, one 128-byte row segment per 8 consecutive lanes (full cache
+//     lines), written to LDS with ds_write_b128 one stage before the MFMAs read it.
+//   * Two LDS buffers, ONE barrier per 64-deep k-step: stage t+1 is written into the buffer that
+//     the previous k-step read (all waves passed that step's barrier after draining their reads)
+//     while the MFMAs of stage t read the other buffer.
+//   * LDS image [row][64] bf16 with the 16-byte chunk XOR-swizzled by (row >> 1) & 7: conflict-free
+//     for the ds_write_b128 groups (8 lanes = one row) and for the ds_read_b128 fragment groups of
+//     both the 16x16x32 and the 32x32x16 MFMA (16 distinct rows per 16-lane group).
+//   * MFMA operands swapped (B fragment as the MFMA's A operand), so a lane holds 4 consecutive
+//     output columns of one row: 8-byte stores with the bias / accumulate fused in the epilogue.
+//   * XCD-aware tile walk: workgroups b, b + 8, ... share an XCD under round-robin dispatch (speed
+//     only); each XCD's tiles form a gm x (tiles / 8 / gm) block so its A and B panels are shared
+//     in the XCD's 4 MB L2.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+typedef h16_t rs_frag __attribute__((ext_vector_type(8)));    // 8 x bf16: one MFMA A/B fragment
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // 16 bytes in 4 VGPRs
+typedef __attribute__((address_space(3))) u32x4 lds_u4t;
+
+struct RsArgs {
+  const bf16_t* a;
+  const bf16_t* b;
+  bf16_t* c;
+  const bf16_t* bias;
+  long lda, ldb, ldc;
+  int M, N, K;
+  int gm;            // m-tiles per group of the XCD-aware walk
+  int accumulate;
+};
+
+DLTB_DEV f32x4 mfma16(rs_frag a, rs_frag b, f32x4 c) {
+#if DLTB_F16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+DLTB_DEV f32x16 mfma32(rs_frag a, rs_frag b, f32x16 c) {
+#if DLTB_F16
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+template <int BM, int BN, int WGM, int D, bool M32>
+struct RsGeo {
+  static_assert(4 % WGM == 0, "4 waves");
+  static constexpr int WGN = 4 / WGM;
+  static constexpr int BK = 64;
+  static constexpr int WM = BM / WGM, WN = BN / WGN;     // wave tile
+  static constexpr int T = M32 ? 32 : 16;                 // MFMA output edge
+  static constexpr int FM = WM / T, FN = WN / T;          // MFMA tiles per wave
+  static constexpr int KS = M32 ? 4 : 2;                  // MFMA k-steps per 64-deep stage
+  static constexpr int NA = BM / 32, NB = BN / 32;        // 16-byte pieces per thread per stage
+  static constexpr int NI = NA + NB;
+  static constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  static constexpr int U = D % 2 == 0 ? D : 2 * D;        // k-loop unroll: register set and LDS buffer both static
+  static constexpr int ACC = M32 ? 16 : 4;
+  static_assert(WM % T == 0 && WN % T == 0 && BM % 32 == 0 && BN % 32 == 0, "tile shape");
+};
+
+// byte offset of 16-byte chunk `ch` of row `row` in a [rows][64] bf16 LDS image
+DLTB_DEV uint32_t rs_off(int row, int ch) { return (uint32_t)(row * 128 + ((ch ^ ((row >> 1) & 7)) << 4)); }
+
+template <int BM, int BN, int WGM, int D, bool M32>
+__global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
+  using G = RsGeo<BM, BN, WGM, D, M32>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WGM, wn = wave / WGM;
+
+  // ---- tile walk: XCD-major, then groups of gm m-tiles x all n-tiles
+  const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  int mb, nb;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {
+    const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  } else {
+    mb = idx / tiles_n;
+    nb = idx - mb * tiles_n;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = g.K / G::BK;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * G::BK == g.K && nk % G::U == 0);
+
+  // ---- staging addresses: piece i of a thread = row 32 i + tid / 8, chunk tid % 8 of the tile
+  const int prow = tid >> 3, pch = tid & 7;
+  const char* abase = (const char*)(g.a + (long)m0 * g.lda);   // wave-uniform
+  const char* bbase = (const char*)(g.b + (long)n0 * g.ldb);
+  uint32_t voa[G::NA], vob[G::NB];
+#pragma unroll
+  for (int i = 0; i < G::NA; ++i) voa[i] = (uint32_t)(((32 * i + prow) * g.lda + pch * 8) * 2);
+#pragma unroll
+  for (int i = 0; i < G::NB; ++i) vob[i] = (uint32_t)(((32 * i + prow) * g.ldb + pch * 8) * 2);
+  const uint32_t wlane = rs_off(prow, pch);   // + 4096 i: rows 32 i + prow keep the swizzle of prow
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+
+  u32x4 R[D][G::NI];
+  auto gload = [&](int kt, u32x4 (&r)[G::NI]) {
+    const int ks = min(kt, nk - 1) * (G::BK * 2);    // past the end: re-read the last stage (never written to a live buffer)
+    const char* pa = abase + ks;
+    const char* pb = bbase + ks;
+#pragma unroll
+    for (int i = 0; i < G::NA; ++i) r[i] = *reinterpret_cast<const u32x4*>(pa + voa[i]);
+#pragma unroll
+    for (int i = 0; i < G::NB; ++i) r[G::NA + i] = *reinterpret_cast<const u32x4*>(pb + vob[i]);
+  };
+  auto swrite = [&](int buf, const u32x4 (&r)[G::NI]) {
+    const uint32_t base = lds0 + buf * G::STAGE + wlane;
+#pragma unroll
+    for (int i = 0; i < G::NA; ++i) *(lds_u4t*)(size_t)(base + 4096 * i) = r[i];
+#pragma unroll
+    for (int i = 0; i < G::NB; ++i) *(lds_u4t*)(size_t)(base + G::A_BYTES + 4096 * i) = r[G::NA + i];
+  };
+
+  // ---- fragment read offsets (lane part; the row base of each fragment is an immediate)
+  // 16x16x32: lane l reads row (l & 15), chunk 4 kk + (l >> 4);  32x32x16: row (l & 31), chunk 2 s + (l >> 5)
+  constexpr int RL = M32 ? 32 : 16;
+  const int fr = lane & (RL - 1), fq = M32 ? (lane >> 5) : (lane >> 4);
+  uint32_t foff[G::KS];
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s) foff[s] = rs_off(fr, (M32 ? 2 : 4) * s + fq);
+  const int arow0 = wm * G::WM, brow0 = wn * G::WN;
+
+  using Acc = typename std::conditional<M32, f32x16, f32x4>::type;
+  Acc acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = Acc{};
+
+  // A k-step's MFMAs in two halves (k 0-31 / 32-63 of the stage), each with its own fragment set
+  // X / Y, so the reads of the next half overlap the MFMAs of the current one.
+  constexpr int KH = G::KS / 2;
+  struct Frags {
+    rs_frag a[KH][G::FM], b[KH][G::FN];
+  };
+  auto fread = [&](Frags& f, int buf, int half) {
+    const uint32_t base = lds0 + buf * G::STAGE;
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+        f.a[s][i] = __builtin_bit_cast(
+            rs_frag, *(lds_u4t*)(size_t)(base + foff[half * KH + s] + (arow0 + G::T * i) * 128));
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j)
+        f.b[s][j] = __builtin_bit_cast(
+            rs_frag, *(lds_u4t*)(size_t)(base + G::A_BYTES + foff[half * KH + s] + (brow0 + G::T * j) * 128));
+    }
+  };
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int s = 0; s < KH; ++s)
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) {
+          if constexpr (M32) acc[i][j] = mfma32(f.b[s][j], f.a[s][i], acc[i][j]);
+          else acc[i][j] = mfma16(f.b[s][j], f.a[s][i], acc[i][j]);
+        }
+  };
+
+  // ---- prologue: D stages in flight; stages 0 and 1 in LDS buffers 0 / 1, stage 0's fragments in X / Y
+  Frags X, Y;
+#pragma unroll
+  for (int d = 0; d < D; ++d) gload(d, R[d]);
+  swrite(0, R[0]);
+  gload(D, R[0]);
+  __syncthreads();                                   // stage 0 visible
+  fread(X, 0, 0);
+  swrite(1, R[1 % D]);
+  gload(D + 1, R[1 % D]);
+  fread(Y, 0, 1);
+  __syncthreads();                                   // stage 1 visible, stage 0's reads drained
+
+  // ---- main loop.  Top of k-step kt: X / Y hold stage kt's fragments, stage kt + 1 is visible in
+  // buffer (kt + 1) & 1 and buffer kt & 1 is free (every wave drained its reads of stage kt before
+  // the barrier); R[(kt + 2) % D] holds stage kt + 2.  Segment: MFMAs of half 0 while the next
+  // stage's half-0 fragments are read and stage kt + 2 is written into the free buffer (its
+  // registers re-issued for stage kt + 2 + D), then MFMAs of half 1 while the half-1 fragments are
+  // read; one barrier.  (Past the end the reads fetch unused data and the writes re-store the last
+  // stage into a buffer nobody reads again.)
+  for (int t = 0; t < nk; t += G::U) {
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const int kt = t + u;
+      mma(X);
+      fread(X, (u + 1) & 1, 0);
+      swrite(u & 1, R[(u + 2) % D]);
+      gload(kt + 2 + D, R[(u + 2) % D]);
+      mma(Y);
+      fread(Y, (u + 1) & 1, 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: lane -> row m, 4 consecutive columns per register group
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+    const int m = m0 + arow0 + G::T * i + fr;
+    bf16_t* crow = g.c + (size_t)m * g.ldc;
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+#pragma unroll
+      for (int q = 0; q < G::ACC / 4; ++q) {
+        // 16x16: columns 4 fq .. +3;  32x32: register group q -> columns 8 q + 4 fq .. +3
+        const int n = n0 + brow0 + G::T * j + (M32 ? 8 * q + 4 * fq : 4 * fq);
+        float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        if (g.bias) {
+          const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
+          v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+        }
+        if (g.accumulate) {
+          const uint2 old = *reinterpret_cast<const uint2*>(crow + n);
+          v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+        }
+        uint2 o;
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(crow + n) = o;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int D, bool M32>
+void launch_rs(const RsArgs& g, hipStream_t st) {
+  constexpr int smem = 2 * RsGeo<BM, BN, WGM, D, M32>::STAGE;
+  static_assert(smem <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_rs_kernel<BM, BN, WGM, D, M32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_rs_kernel<BM, BN, WGM, D, M32>), dim3(tiles), dim3(256), smem, st, g);
+}
+
+struct RsCfg {
+  int bm, bn, wgm, d;
+  bool m32;
+};
+// 0-2: N = 1024 products (16 x 16 tiles of 128 x 64); 3-4 / 6: N = 4096 (128 x 256); 5: N = 3072 (128 x 192)
+constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {128, 64, 2, 2, true},
+                             {128, 256, 2, 2, false}, {128, 256, 2, 2, true}, {128, 192, 2, 2, false},
+                             {128, 128, 2, 2, false}, {64, 128, 2, 2, false}};
+constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
+
+void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
+  switch (cfg) {
+    case 0: launch_rs<128, 64, 2, 2, false>(g, st); break;
+    case 1: launch_rs<128, 64, 2, 4, false>(g, st); break;
+    case 2: launch_rs<128, 64, 2, 2, true>(g, st); break;
+    case 3: launch_rs<128, 256, 2, 2, false>(g, st); break;
+    case 4: launch_rs<128, 256, 2, 2, true>(g, st); break;
+    case 5: launch_rs<128, 192, 2, 2, false>(g, st); break;
+    case 6: launch_rs<128, 128, 2, 2, false>(g, st); break;
+    default: launch_rs<64, 128, 2, 2, false>(g, st); break;
+  }
+}
+
+}  // namespace
+
+static bool rs_fits(int c, int M, int N, int K) {
+  if (c < 0 || c >= kRsNumCfgs) return false;
+  const RsCfg t = kRsCfgs[c];
+  const int u = t.d % 2 == 0 ? t.d : 2 * t.d;
+  return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % 64 == 0 && (K / 64) % u == 0;
+}
+
+int dltb_gemm_rs_pick(int M, int N, int K) {
+  // the config whose tile count is closest to one workgroup per CU (256); ties keep the earlier
+  int best = -1, bestd = 1 << 30;
+  for (int c = 0; c < kRsNumCfgs; ++c) {
+    if (!rs_fits(c, M, N, K)) continue;
+    const int tiles = (M / kRsCfgs[c].bm) * (N / kRsCfgs[c].bn);
+    const int d = tiles > 256 ? (tiles - 256) * 2 : 256 - tiles;
+    if (d < bestd) {
+      bestd = d;
+      best = c;
+    }
+  }
+  return best;
+}
+
+bool dltb_gemm_rs_supported(int M, int N, int K, int cfg) {
+  if (cfg < 0) cfg = dltb_gemm_rs_pick(M, N, K);
+  return rs_fits(cfg, M, N, K);
+}
+
+int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st) {
+  if (cfg < 0) cfg = dltb_gemm_rs_pick(M, N, K);
+  if (!dltb_gemm_rs_supported(M, N, K, cfg)) return -1;
+  RsArgs g{};
+  g.a = (const bf16_t*)a;
+  g.b = (const bf16_t*)b;
+  g.c = (bf16_t*)c;
+  g.bias = (const bf16_t*)bias;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.gm = gm;
+  g.accumulate = accumulate;
+  launch_rs_cfg(cfg, g, st);
+  return cfg;
+}

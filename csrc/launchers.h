@@ -160,6 +160,12 @@ int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long l
                  int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part = nullptr,
                  int* sync = nullptr);
 
+// ---- gemm_rs.hip: the same NT product with register-staged operands (the step's per-layer kernel)
+int dltb_gemm_rs_pick(int M, int N, int K);
+bool dltb_gemm_rs_supported(int M, int N, int K, int cfg);
+int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st);
+
 // device-scalar helpers (head backward: no host sync)
 void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,
                     hipStream_t st);

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Locate wrong output tiles of gemm_rs: per config and shape, the (m-tile, n-tile) blocks whose max error
+exceeds the tolerance, over repeated launches (debug aid for the register-staged GEMM)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import dltb  # noqa: E402,F401
+from dltb.ops._ext import ext  # noqa: E402
+
+TILE = {0: (128, 64), 1: (128, 64), 2: (128, 64), 3: (128, 256), 4: (128, 256), 5: (128, 192), 6: (128, 128),
+        7: (64, 128)}
+C = ext()
+torch.manual_seed(0)
+for (M, N, K) in [(2048, 1024, 1024), (2048, 3072, 1024), (6144, 1024, 1024), (2048, 2048, 1024),
+                  (4096, 1024, 1024), (2048, 1024, 256)]:
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    for c in (0, 6, 7):
+        if not C.gemm_rs_supported(M, N, K, c):
+            continue
+        bm, bn = TILE[c]
+        bad = set()
+        nbad_runs = 0
+        for rep in range(5):
+            y = C.gemm_rs(x, w, None, None, False, c, 1)
+            torch.cuda.synchronize()
+            e = (y.float() - ref).abs().reshape(M // bm, bm, N // bn, bn).amax(dim=(1, 3))
+            b = (e > 0.05).nonzero().tolist()
+            nbad_runs += bool(b)
+            bad |= {tuple(t) for t in b}
+        tiles = (M // bm) * (N // bn)
+        ex = sorted(bad)[:12]
+        print(f"M{M} N{N} K{K} c{c} tiles {tiles}: bad runs {nbad_runs}/5, bad tiles {len(bad)} e.g. {ex}", flush=True)
+        if bad:
+            # which rows / cols inside a bad tile
+            y = C.gemm_rs(x, w, None, None, False, c, 1)
+            torch.cuda.synchronize()
+            mb, nb = sorted(bad)[0]
+            d = (y.float() - ref)[mb * bm:(mb + 1) * bm, nb * bn:(nb + 1) * bn].abs() > 0.05
+            rows = d.any(1).nonzero().flatten().tolist()
+            cols = d.any(0).nonzero().flatten().tolist()
+            print(f"   tile {mb},{nb}: bad rows {rows[:40]} ({len(rows)}), bad cols {cols[:40]} ({len(cols)})", flush=True)
