@@ -118,6 +118,14 @@ class FlatAdamW:
         blocks of a segment are contiguous rows).  With ``prepare`` called once per step, the
         per-segment launches together are exactly ``launch`` -- the engine uses them to let each
         bucket's forward wait for its own parameters only."""
+        if not self.master.is_cuda:              # CPU reference: the same update on the segment's rows
+            b1, b2 = self.betas
+            ostart, length, dst = self.segments[i]
+            sl = slice(ostart, ostart + length)
+            ref.adamw_flat(self.master[sl], self.exp_avg[sl], self.exp_avg_sq[sl], grad[sl], self._lr_now, b1, b2,
+                           self.eps, self.weight_decay, self.step_count, gscale)
+            dst.copy_(self.master[sl])
+            return
         lo, hi = self._seg_blocks[i]
         self._launch_rows(lo, hi, grad, gscale)
 

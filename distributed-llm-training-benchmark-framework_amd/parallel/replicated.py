@@ -140,6 +140,22 @@ class ReplicatedEngine(Engine):
             master = master_full
             opt_segs = [(0, L.total, self.flat_param)]
             self.rs_out = self.acc = None
+        # DDP at world > 1 without a loss scaler and without clipping (the reference's DDP in bf16:
+        # train_harness.py:210-223 + :328-329 -- AdamW on every micro-step, no clip, no schedule):
+        # the optimizer is pipelined under the all-reduce tail.  Each bucket is one AdamW segment;
+        # the update waits for its OWN bucket's all-reduce only (a device-side stream wait), so the
+        # buckets reduced early in the backward are updated while the last ones are still on the
+        # wire and only the last bucket's rows stay exposed behind the comm tail.  (fp16 with dynamic
+        # loss scaling needs the global inf check over every bucket first, and clipping the global
+        # norm: both keep the whole-model update after the last wait.)
+        self._ddp_pipe = (self.stage == 0 and self.world > 1 and self._overlap and self.scaler is None
+                          and not cfg.grad_clip > 0 and not cfg.extra.get("track_grad_norm", False)
+                          and os.environ.get("DLTB_DDP_OPT_PIPELINE", "1") == "1")
+        self._ar_works = {}      # bucket -> its all-reduce (untracked) while the pipeline is on
+        if self._ddp_pipe:
+            g_full = self.comm_f32 if self.comm_f32 is not None else self.flat_grad
+            opt_segs = [(bk.start, bk.end - bk.start, self.flat_param[bk.start:bk.end]) for bk in L.buckets]
+            assert sum(x[1] for x in opt_segs) == g_full.numel() == L.total
         del master_full
         self.opt = FlatAdamW(master, opt_segs, cfg.lr, cfg.betas, cfg.eps, cfg.weight_decay)
         self._ag_pending = {}    # bucket -> async all-gather of updated parameters (deferred step)
@@ -356,7 +372,9 @@ class ReplicatedEngine(Engine):
                     ext().f32_from_bf16_(c, g, False)
                 else:
                     c.copy_(g)
-                self.comm.all_reduce(c, async_op=not sync)
+                g = c
+            if self._ddp_pipe:       # waited by its own AdamW segment (or the token rows), not wait_all
+                self._ar_works[b] = self.comm.all_reduce(g, async_op=True, track=False)
             else:
                 self.comm.all_reduce(g, async_op=not sync)
         elif not self._use_rs:
@@ -433,6 +451,7 @@ class ReplicatedEngine(Engine):
             b = self._bucket_of[id(self._sparse[0][0])]
             if b in self._rs_inflight:
                 self._drain_bucket(b)          # the token table's chunk, then its sparse rows
+            self._wait_allreduce(b)            # (DDP pipeline: the rows add into the reduced bucket)
             if self._sparse is not None:
                 self._apply_sparse()
         # (ZeRO-2 inside a window: the row all-gathers stay in flight with the table's reduce-
@@ -457,7 +476,21 @@ class ReplicatedEngine(Engine):
             return self.acc
         return self.rs_out if self.world > 1 else self.flat_grad
 
+    def _wait_allreduce(self, b):
+        w = self._ar_works.pop(b, None)
+        if w is not None:
+            w.wait()
+
     def _update(self, lr):
+        if self._ddp_pipe:
+            # per bucket, in all-reduce issue order: wait for that bucket's sum, then its AdamW rows
+            g = self._owner_grad()
+            gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)   # (no clip: a fill)
+            self.opt.prepare(lr)
+            for b in range(len(self.layout.buckets)):
+                self._wait_allreduce(b)
+                self.opt.launch_segment(b, g, gscale)
+            return
         self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
 
     def _deferred_optimizer_step(self, lr):
@@ -516,6 +549,8 @@ class ReplicatedEngine(Engine):
                     self.comm.broadcast(full[r * bk.chunk:(r + 1) * bk.chunk], src=self.comm.global_rank(r))
 
     def _wait_param_gathers(self):
+        for b in list(self._ar_works):
+            self._wait_allreduce(b)
         self._drain_all()
         for w in self._ag_pending.values():
             w.wait()
