@@ -166,10 +166,10 @@ def resolve_precision(args):
     """--dtype / --grad-comm-dtype auto -> the reference's precision per strategy (harness.py)."""
     if args.dtype == "auto":
         args.dtype = "fp16" if args.strategy in ("ddp", "fsdp") else "bf16"
-        if args.strategy in ("zero2", "zero3") and args.deepspeed_config:   # the config's precision
+        if args.strategy in ("zero2", "zero3"):   # the DeepSpeed config's precision (the default one as the harness)
             from dltb.parallel.ds_config import ds_precision
-            from dltb.parallel.strategy import load_deepspeed_config
-            args.dtype = ds_precision(load_deepspeed_config(args.deepspeed_config))
+            from dltb.parallel.strategy import default_config_path, load_deepspeed_config
+            args.dtype = ds_precision(load_deepspeed_config(args.deepspeed_config or default_config_path(args.strategy)))
     if args.grad_comm_dtype == "auto":
         args.grad_comm_dtype = "fp32" if (args.strategy == "ddp" and args.dtype == "fp16") else "compute"
     return args

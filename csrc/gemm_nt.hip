@@ -474,6 +474,10 @@ int dltb_gemm_nt_fixup_ints(int cfg, int M, int N) {
 
 bool dltb_gemm_nt_supported(int M, int N, int K, int cfg) {
   if (cfg < 0) cfg = dltb_gemm_nt_pick(M, N, K);
+  // the split-K pair fixup (cfg 10) polls a flag with a bounded spin and would add unready partials
+  // after a timeout: an A/B-only config, refused unless DLTB_NT_FIXUP_AB=1
+  static const bool fixup_ab = getenv("DLTB_NT_FIXUP_AB") && atoi(getenv("DLTB_NT_FIXUP_AB")) == 1;
+  if (cfg >= 0 && cfg < kNtNumCfgs && kNtCfgs[cfg].fix && !fixup_ab) return false;
   return cfg >= 0 && cfg < kNtNumCfgs && nt_fits(cfg, M, N, K);
 }
 

@@ -180,7 +180,12 @@ class ShardedEngine(Engine):
         # backward; the next backward's first gradient write waits for them and folds the chunks into
         # the fp32 accumulator (one launch), a forward later, when they are long done.  The window's
         # last micro-step drains everything before the optimizer (as the replicated engines do).
-        self._tail_defer = (self.world > 1 and self.acc is not None and self._overlap and
+        # (resident group gradient buffers only, models below 2B parameters: with the transient
+        # per-micro-step buffers of a larger model, deferring the drain would keep a full model of
+        # bf16 gradients alive through the next forward -- ~14.5 GB per rank at Mistral-7B -- which
+        # DeepSpeed / torch FSDP free at the end of the backward)
+        self._grad_resident = sum(u.numel for u in self.model.units()) < 2_000_000_000
+        self._tail_defer = (self.world > 1 and self.acc is not None and self._overlap and self._grad_resident and
                             bool(cfg.extra.get("defer_tail_reduce", True)))
         self._rs_inflight = []       # reduce-scatter works of the current / deferred micro-step
         self._deferred = False       # a finished micro-step's reduce-scatters are still to be drained
@@ -201,8 +206,8 @@ class ShardedEngine(Engine):
         self._pool_on = os.environ.get("DLTB_GATHER_POOL", "1") == "1"      # A/B toggle
         self._gviews = {}            # (id(unit), i) -> (gradient slot view, its group or None)
         # resident group gradient buffers at world > 1 for models below 2B parameters (a full model's
-        # worth of bf16 gradients per rank: 0.47 GB at TinyGPT-A; Mistral-7B keeps transient ones)
-        self._grad_resident = sum(u.numel for u in self.model.units()) < 2_000_000_000
+        # worth of bf16 gradients per rank: 0.47 GB at TinyGPT-A; Mistral-7B keeps transient ones):
+        # self._grad_resident, set above
         self._reduced = set()        # group ids reduce-scattered in this micro-step
         self._p_reduced = False      # the persistent block reduce-scattered in this micro-step
         self._sparse = None          # (token slot, persistent?, gathered rows, gathered ids, works)
@@ -676,6 +681,10 @@ class ShardedEngine(Engine):
                 # per-window W^T copies of the NT-form data-gradient GEMMs.  peak_vram_gb includes them.
                 "resident_grad_bytes": sum(g.grad_buf.numel() * e for g in self.groups
                                            if g.grad_buf is not None and self.world > 1),
+                # transient gradient buffers still referenced after their reduce-scatter was issued
+                # (freed when it is waited; with the tail deferral only resident buffers are held)
+                "held_grad_bytes": sum(t.numel() * t.element_size() for t in self._held_grads
+                                       if not any(t is g.grad_buf for g in self.groups)),
                 "weight_t_cache_bytes": sum(t.numel() * t.element_size() for t, _ in (self._wt_multi or {}).values()),
                 "gather_pool_bytes": sum(b.numel() * e for bufs in self._gpool.values() for b in bufs)}
 

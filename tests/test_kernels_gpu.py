@@ -313,7 +313,7 @@ def test_gemm_nt_pair_fixup(M, N, K):
     C_ = ext()
     cfg = 10
     if not C_.gemm_nt_supported(M, N, K, cfg):
-        pytest.skip("tile config does not divide this shape")
+        pytest.skip("cfg 10 is A/B-only (DLTB_NT_FIXUP_AB=1) or does not divide this shape")
     a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
     a = a_full[:, 32:K + 32]
     bias = rnd(N)
