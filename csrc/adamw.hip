@@ -13,17 +13,17 @@
 //                                p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // with g optionally multiplied by a device-side scale (gradient clipping coefficient / 1/accum),
 // read from memory so no host sync is needed.
-#include "common.h"
+#include <cstdlib>
 
-#ifndef DLTB_ADAM_ITERS       // vectors of 4 per thread (A/B knob: 2 -> +2 %, 8 -> 4x slower, spills)
-#define DLTB_ADAM_ITERS 4
-#endif
+#include "common.h"
 
 namespace {
 
 constexpr int kAdamThreads = 256;
-constexpr int kAdamIters = DLTB_ADAM_ITERS;
-constexpr int kAdamChunk = kAdamThreads * 4 * kAdamIters;   // elements per block
+constexpr int kAdamChunk = kAdamThreads * 16;   // elements per block (host block tables)
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 template <typename G>
 DLTB_DEV void load4(const G* p, float* g);
@@ -37,6 +37,94 @@ DLTB_DEV void load4<bf16_t>(const bf16_t* p, float* g) {
   uint2 v = *reinterpret_cast<const uint2*>(p);
   g[0] = lo_bf(v.x); g[1] = hi_bf(v.x); g[2] = lo_bf(v.y); g[3] = hi_bf(v.y);
 }
+// 8 gradient elements: one 16-byte load for 16-bit gradients, two for fp32
+template <typename G>
+DLTB_DEV void load8(const G* p, float* g);
+template <>
+DLTB_DEV void load8<float>(const float* p, float* g) {
+  const v4f a = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+  const v4f b = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p + 4));
+  g[0] = a[0]; g[1] = a[1]; g[2] = a[2]; g[3] = a[3]; g[4] = b[0]; g[5] = b[1]; g[6] = b[2]; g[7] = b[3];
+}
+template <>
+DLTB_DEV void load8<bf16_t>(const bf16_t* p, float* g) {
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  g[0] = lo_bf(v[0]); g[1] = hi_bf(v[0]); g[2] = lo_bf(v[1]); g[3] = hi_bf(v[1]);
+  g[4] = lo_bf(v[2]); g[5] = hi_bf(v[2]); g[6] = lo_bf(v[3]); g[7] = hi_bf(v[3]);
+}
+
+struct AdamHp {
+  float lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, gs;
+};
+
+DLTB_DEV void adam_elem(float& p, float& m, float& v, float g, const AdamHp& h) {
+  const float gg = g * h.gs;
+  p *= 1.f - h.lr * h.wd;
+  m = m + (1.f - h.beta1) * (gg - m);
+  v = h.beta2 * v + (1.f - h.beta2) * gg * gg;
+  const float denom = sqrtf(v) * h.inv_sqrt_bc2 + h.eps;
+  p -= h.step_size * m / denom;
+}
+
+// W elements per lane and vector access (8: every stream moved in 16-byte accesses -- master /
+// moments as two float4, a 16-bit gradient and the 16-bit parameter copy as one 16-byte access;
+// 4: the 8-byte 16-bit accesses of segments not 8-element aligned).  ITERS vectors per lane, all
+// loads issued before the first update (ITERS * (6 + 1) 16-byte loads in flight per lane at W = 8).
+template <typename G, int W>
+DLTB_DEV void adamw_block(float* __restrict__ master, float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
+                          const G* __restrict__ grad, bf16_t* __restrict__ dst, int64_t start, int64_t seg_end,
+                          int64_t dst_base, const AdamHp& h) {
+  constexpr int ITERS = kAdamChunk / (kAdamThreads * W);
+  constexpr int NV = W / 4;
+  v4f P[ITERS][NV], M[ITERS][NV], V[ITERS][NV];
+  float Gr[ITERS][W];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int64_t i = start + ((int64_t)it * kAdamThreads + threadIdx.x) * W;
+    if (i < seg_end) {
+#pragma unroll
+      for (int q = 0; q < NV; ++q) {
+        P[it][q] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(master + i + 4 * q));
+        M[it][q] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(exp_avg + i + 4 * q));
+        V[it][q] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(exp_avg_sq + i + 4 * q));
+      }
+      if constexpr (W == 8) load8<G>(grad + i, Gr[it]);
+      else load4<G>(grad + i, Gr[it]);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int64_t off = ((int64_t)it * kAdamThreads + threadIdx.x) * W;
+    const int64_t i = start + off;
+    if (i >= seg_end) break;
+    float p[W], m[W], v[W];
+#pragma unroll
+    for (int e = 0; e < W; ++e) {
+      p[e] = P[it][e >> 2][e & 3];
+      m[e] = M[it][e >> 2][e & 3];
+      v[e] = V[it][e >> 2][e & 3];
+      adam_elem(p[e], m[e], v[e], Gr[it][e], h);
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      __builtin_nontemporal_store((v4f){p[4 * q], p[4 * q + 1], p[4 * q + 2], p[4 * q + 3]},
+                                  reinterpret_cast<v4f*>(master + i + 4 * q));
+      __builtin_nontemporal_store((v4f){m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]},
+                                  reinterpret_cast<v4f*>(exp_avg + i + 4 * q));
+      __builtin_nontemporal_store((v4f){v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]},
+                                  reinterpret_cast<v4f*>(exp_avg_sq + i + 4 * q));
+    }
+    if constexpr (W == 8) {
+      v4u o = {pack_bf2(p[0], p[1]), pack_bf2(p[2], p[3]), pack_bf2(p[4], p[5]), pack_bf2(p[6], p[7])};
+      *reinterpret_cast<v4u*>(dst + dst_base + off) = o;
+    } else {
+      uint2 o;
+      o.x = pack_bf2(p[0], p[1]);
+      o.y = pack_bf2(p[2], p[3]);
+      *reinterpret_cast<uint2*>(dst + dst_base + off) = o;
+    }
+  }
+}
 
 template <typename G>
 __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
@@ -44,7 +132,7 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
     const G* __restrict__ grad, const int* __restrict__ blk_seg, const int64_t* __restrict__ blk_start,
     const int64_t* __restrict__ seg_ostart, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, const float* __restrict__ hp,
-    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2) {
+    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int narrow) {
   if (hp) {   // step-dependent hyper-parameters from device memory (HIP-graph replays)
     if (hp[3] != 0.f) return;   // dynamic loss scaling found an inf / nan: the step is skipped
     lr = hp[0];
@@ -53,55 +141,18 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
   }
   const int seg = blk_seg[blockIdx.x];
   const int64_t start = blk_start[blockIdx.x];
-  const int64_t seg_end = seg_ostart[seg] + seg_len[seg];
-  DLTB_DCHECK(seg >= 0 && start >= seg_ostart[seg] && start < seg_end);
+  const int64_t s0 = seg_ostart[seg];
+  const int64_t seg_end = s0 + seg_len[seg];
+  DLTB_DCHECK(seg >= 0 && start >= s0 && start < seg_end);
   bf16_t* dst = reinterpret_cast<bf16_t*>(seg_dst[seg]);
-  const int64_t dst_base = start - seg_ostart[seg];
-  const float gs = gscale ? *gscale : 1.f;
-  const float decay = 1.f - lr * wd;
+  const int64_t dst_base = start - s0;
+  const AdamHp h{lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, gscale ? *gscale : 1.f};
   // every state element is touched once per step: streamed past the caches (nontemporal loads and
-  // stores), and all of a thread's loads are issued before the first update: 1212 -> 1125 us per
-  // step at TinyGPT-A's 236M parameters (profiles/adamw_nontemporal_r2.txt)
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  v4f P4[kAdamIters], M4[kAdamIters], V4[kAdamIters];
-  float G4[kAdamIters][4];
-#pragma unroll
-  for (int it = 0; it < kAdamIters; ++it) {
-    const int64_t i = start + (int64_t)it * kAdamThreads * 4 + threadIdx.x * 4;
-    if (i < seg_end) {
-      P4[it] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(master + i));
-      M4[it] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(exp_avg + i));
-      V4[it] = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(exp_avg_sq + i));
-      load4<G>(grad + i, G4[it]);
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < kAdamIters; ++it) {
-    const int64_t off = (int64_t)it * kAdamThreads * 4 + threadIdx.x * 4;
-    const int64_t i = start + off;
-    if (i >= seg_end || off >= kAdamChunk) break;
-    float p[4], g[4], m[4], v[4];
-    p[0] = P4[it][0]; p[1] = P4[it][1]; p[2] = P4[it][2]; p[3] = P4[it][3];
-    m[0] = M4[it][0]; m[1] = M4[it][1]; m[2] = M4[it][2]; m[3] = M4[it][3];
-    v[0] = V4[it][0]; v[1] = V4[it][1]; v[2] = V4[it][2]; v[3] = V4[it][3];
-    g[0] = G4[it][0]; g[1] = G4[it][1]; g[2] = G4[it][2]; g[3] = G4[it][3];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gg = g[e] * gs;
-      p[e] *= decay;
-      m[e] = m[e] + (1.f - beta1) * (gg - m[e]);
-      v[e] = beta2 * v[e] + (1.f - beta2) * gg * gg;
-      const float denom = sqrtf(v[e]) * inv_sqrt_bc2 + eps;
-      p[e] -= step_size * m[e] / denom;
-    }
-    __builtin_nontemporal_store((v4f){p[0], p[1], p[2], p[3]}, reinterpret_cast<v4f*>(master + i));
-    __builtin_nontemporal_store((v4f){m[0], m[1], m[2], m[3]}, reinterpret_cast<v4f*>(exp_avg + i));
-    __builtin_nontemporal_store((v4f){v[0], v[1], v[2], v[3]}, reinterpret_cast<v4f*>(exp_avg_sq + i));
-    uint2 o;
-    o.x = pack_bf2(p[0], p[1]);
-    o.y = pack_bf2(p[2], p[3]);
-    *reinterpret_cast<uint2*>(dst + dst_base + off) = o;
-  }
+  // stores).  16-byte accesses need 8-element alignment of the owner offset, the segment length and
+  // the destination (wave-uniform test per block; the layouts align segments to 128 elements)
+  const bool wide = !narrow && ((s0 | seg_len[seg]) & 7) == 0 && (((uintptr_t)dst) & 15) == 0;
+  if (wide) adamw_block<G, 8>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
+  else adamw_block<G, 4>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
 }
 
 // sum of squares in a FIXED order (bitwise reproducible: eager runs, graph replays and ranks agree):
@@ -212,14 +263,15 @@ void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* gr
                 float lr, float beta1, float beta2, float eps, float wd, float step_size,
                 float inv_sqrt_bc2, hipStream_t st) {
   if (nblocks <= 0) return;
+  static const int narrow = getenv("DLTB_ADAM_NARROW") ? atoi(getenv("DLTB_ADAM_NARROW")) : 0;   // A/B: 8-byte path
   if (grad_bf16)
     hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
                        exp_avg, exp_avg_sq, (const bf16_t*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, narrow);
   else
     hipLaunchKernelGGL(adamw_kernel<float>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
                        exp_avg, exp_avg_sq, (const float*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, narrow);
 }
 
 int dltb_sumsq_partials() { return kSumsqBlocks; }

@@ -523,6 +523,26 @@ def test_adamw_matches_torch(gdtype):
     close(out_bf16, tp.detach().to(torch.bfloat16), 1e-2, 1e-2, "adamw bf16 copy")
 
 
+def test_adamw_mixed_alignment_segments():
+    """FlatAdamW over two segments, the second neither 8-element aligned in the owner space nor 16-byte
+    aligned at its destination: its blocks take the 8-byte path, the first segment's the 16-byte path;
+    both match torch.optim.AdamW."""
+    from dltb.optim.adamw import FlatAdamW
+    n, cut = 100_000, 50_004
+    p0 = torch.randn(n, device=DEV)
+    out_bf16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+    opt = FlatAdamW(p0.clone(), [(0, cut, out_bf16[:cut]), (cut, n - cut, out_bf16[cut:])], lr=1e-3)
+    tp = torch.nn.Parameter(p0.clone())
+    ref = torch.optim.AdamW([tp], lr=1e-3, weight_decay=0.01)
+    for _ in range(3):
+        g = torch.randn(n, device=DEV).to(torch.bfloat16)
+        tp.grad = g.float()
+        ref.step()
+        opt.step(g, 1e-3)
+    close(opt.master, tp.detach(), 1e-6, 1e-5, "adamw master (two segments)")
+    close(out_bf16, tp.detach().to(torch.bfloat16), 1e-2, 1e-2, "adamw bf16 copy (two segments)")
+
+
 def test_sumsq_clip():
     C = ext()
     x = torch.randn(1 << 20, device=DEV)
