@@ -25,7 +25,10 @@
 # Like the reference it always exits 0; failed configs are listed in results/summary/failures.json.
 #
 #   ./scripts/run_all_benchmarks.sh [results-dir]
-#   env: STEPS, SEQ, TIER, WS_LIST, STRATS, TIMEOUT, HARNESS_EXTRA (extra harness flags),
+#   env: STEPS, SEQ, SEQ_LIST (several sequence lengths: the vram_vs_seqlen plot), TIER, WS_LIST, STRATS,
+#        BENCHMARKS / BENCHMARKS_FILE (explicit "STRATEGY WS SEQ TIER STEPS" rows instead of the
+#        STRATS x SEQ_LIST x WS_LIST product, e.g. configs/suite/multiseq_1gpu.txt), TIMEOUT,
+#        HARNESS_EXTRA (extra harness flags),
 #        M7B, M7B_WS, M7B_TIER, M7B_SEQ, M7B_STEPS (step 2b),
 #        FORCE_NPROC (process slots when no GPU is visible, e.g. the gloo/CPU rehearsal),
 #        COLLECTIVES=0 (skip step 1), COLL_MAX_MB (largest swept message, default 512)
@@ -95,23 +98,39 @@ variant() {   # row name -> "engine strategy|extra harness flags"
     *) echo "" ;;
   esac
 }
-for s in $STRATS; do
+# rows "STRATEGY WS SEQ TIER STEPS" (the reference's BENCHMARKS matrix, run_all_benchmarks.sh:32-52): from
+# BENCHMARKS_FILE / BENCHMARKS (one row per line, '#' comments) when given, else STRATS x SEQ_LIST x WS_LIST
+ROWS=()
+if [[ -n "${BENCHMARKS_FILE:-}" ]]; then BENCHMARKS="$(cat "$BENCHMARKS_FILE")"; fi
+if [[ -n "${BENCHMARKS:-}" ]]; then
+  while IFS= read -r line; do
+    line="${line%%#*}"; read -r -a f <<< "$line"
+    [[ ${#f[@]} -eq 0 ]] && continue
+    [[ ${#f[@]} -ne 5 ]] && { echo "bad matrix row: $line"; FAILED+=("matrix-row"); continue; }
+    ROWS+=("${f[*]}")
+  done <<< "$BENCHMARKS"
+else
+  for s in $STRATS; do for seq in ${SEQ_LIST:-$SEQ}; do for ws in $WS_LIST; do
+    ROWS+=("$s $ws $seq $TIER $STEPS")
+  done; done; done
+fi
+for row in "${ROWS[@]}"; do
+  read -r s ws seq tier steps <<< "$row"
   spec="$(variant "$s")"
   if [[ -z "$spec" ]]; then echo "unknown row $s"; FAILED+=("$s"); continue; fi
   eng="${spec%%|*}"; read -r -a VX <<< "${spec#*|}"
-  for ws in $WS_LIST; do
-    if [[ "$ws" -gt "$NGPU" ]]; then echo "skip $s ws=$ws (only $NGPU GPUs)"; continue; fi
-    job="bench-master-${s}-ws${ws}-seq${SEQ}"
-    echo "---- $job"
-    if timeout -k 30 "$TIMEOUT" "$ROOT/scripts/launch_local.sh" --strategy "$eng" --world-size "$ws" --seq-len "$SEQ" \
-         --tier "$TIER" --steps "$STEPS" --per-device-batch 1 --grad-accum 4 --results-dir "$RESULTS/raw" \
-         -- "${VX[@]}" "${HX[@]}" > "$RESULTS/$job.log" 2>&1 \
-       && "$ROOT/scripts/collect_results.sh" "$RESULTS/$job.log" "$RESULTS" "$job" "$RESULTS/raw"; then
-      DONE=$((DONE + 1)); echo "     ok"
-    else
-      FAILED+=("$job"); echo "     FAILED (see $RESULTS/$job.log)"; tail -20 "$RESULTS/$job.log" || true
-    fi
-  done
+  if [[ "$ws" -gt "$NGPU" ]]; then echo "skip $s ws=$ws (only $NGPU GPUs)"; continue; fi
+  job="bench-master-${s}-ws${ws}-seq${seq}"
+  [[ "$tier" != "$TIER" ]] && job="${job}-tier${tier}"
+  echo "---- $job"
+  if timeout -k 30 "$TIMEOUT" "$ROOT/scripts/launch_local.sh" --strategy "$eng" --world-size "$ws" --seq-len "$seq" \
+       --tier "$tier" --steps "$steps" --per-device-batch 1 --grad-accum 4 --results-dir "$RESULTS/raw" \
+       -- "${VX[@]}" "${HX[@]}" > "$RESULTS/$job.log" 2>&1 \
+     && "$ROOT/scripts/collect_results.sh" "$RESULTS/$job.log" "$RESULTS" "$job" "$RESULTS/raw"; then
+    DONE=$((DONE + 1)); echo "     ok"
+  else
+    FAILED+=("$job"); echo "     FAILED (see $RESULTS/$job.log)"; tail -20 "$RESULTS/$job.log" || true
+  fi
 done
 # ---- 2b. BASELINE config #5: Mistral-7B-shape ZeRO-3 at 1 and 8 GPUs
 if [[ "${M7B:-1}" != "0" ]]; then

@@ -9,10 +9,10 @@ import pandas as pd
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _suite(tmp_path, extra, strats="ddp zero2", m7b="0"):
+def _suite(tmp_path, extra, strats="ddp zero2", m7b="0", **more):
     env = dict(os.environ, STEPS="6", SEQ="64", TIER="tiny", WS_LIST="1 2", STRATS=strats, FORCE_NPROC="2",
                HARNESS_EXTRA=f"--device cpu --warmup-steps 2 --log-every 0 {extra}", TIMEOUT="300",
-               OMP_NUM_THREADS="1", M7B=m7b, M7B_TIER="mtiny", M7B_SEQ="64", M7B_STEPS="6", M7B_WS="1 2")
+               OMP_NUM_THREADS="1", M7B=m7b, M7B_TIER="mtiny", M7B_SEQ="64", M7B_STEPS="6", M7B_WS="1 2", **more)
     r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "run_all_benchmarks.sh"), str(tmp_path)],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -70,3 +70,27 @@ def test_suite_m7b_rows(tmp_path):
     assert json.load(open(tmp_path / "summary" / "failures.json")) == {"failed": []}
     ext = json.load(open(tmp_path / "bench-master-zero3_m7b_288gb-ws2-seq64_results" / "result.extended.json"))
     assert ext["trainable_params"] > 0 and ext["peak_vram_reserved_gb"] is not None
+
+
+def test_suite_multi_seq_matrix(tmp_path):
+    """Per-row matrix ("STRATEGY WS SEQ TIER STEPS", the reference's BENCHMARKS format) with several sequence
+    lengths and a row of another tier: every row lands in the CSV with its seq_len, and plot.py draws the
+    conditional vram_vs_seqlen.png next to the other four plots (reference plot.py:56-71)."""
+    rows = "zero2 1 32 tiny 6\nzero2 1 64 tiny 6\nddp 1 32 tiny 6\nddp 1 64 tiny 6\n# comment\nzero3 1 64 mtiny 6\n"
+    _suite(tmp_path, "", BENCHMARKS=rows)
+    df = pd.read_csv(tmp_path / "summary" / "metrics.csv")
+    assert sorted(zip(df.strategy, df.seq_len)) == [("ddp", 32), ("ddp", 64), ("zero2", 32), ("zero2", 64),
+                                                    ("zero3", 64)]
+    assert json.load(open(tmp_path / "summary" / "failures.json")) == {"failed": []}
+    plots = {p.name for p in (tmp_path / "summary" / "plots").iterdir()}
+    assert plots == {"tokens_per_sec_vs_gpu.png", "step_time_vs_gpu.png", "vram_vs_seqlen.png",
+                     "scaling_efficiency.png", "gbps_vs_gpu.png"}
+    assert (tmp_path / "bench-master-zero3-ws1-seq64-tiermtiny_results" / "result.json").exists()
+
+
+def test_shipped_multiseq_matrix_parses():
+    rows = [ln.split("#")[0].split() for ln in open(os.path.join(ROOT, "configs", "suite", "multiseq_1gpu.txt"))]
+    rows = [r for r in rows if r]
+    assert all(len(r) == 5 for r in rows)
+    assert {int(r[2]) for r in rows} == {2048, 4096, 8192}
+    assert ["fsdp", "1", "4096", "B", "100"] in rows and ["zero3", "1", "8192", "B", "100"] in rows
