@@ -76,6 +76,9 @@ def build_parser():
                     help="DeepSpeed JSON for zero2/zero3 (default configs/deepspeed/<strategy>.json)")
     ap.add_argument("--fsdp-wrap", default="block", choices=["block", "root"],
                     help="FSDP unit layout: per transformer block, or the reference's single root FlatParameter")
+    ap.add_argument("--fsdp-sharding", default=None, choices=["full_shard", "shard_grad_op"],
+                    help="FSDP sharding_strategy (default: configs/fsdp/fsdp_config.yaml's full_shard); "
+                         "shard_grad_op keeps the gathered parameters from forward to backward (no re-gather)")
     ap.add_argument("--graphs", default="auto", choices=["auto", "on", "off"],
                     help="replay each micro-step as a captured HIP graph (DLTB_GRAPHS overrides)")
     ap.add_argument("--tunableop", default="auto", choices=["auto", "use", "tune", "off"],
@@ -223,7 +226,7 @@ def run_rank(args) -> int:
                                grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype=args.dtype,
                                bucket_mb=bucket_mb, seed=42, grad_reduce=args.grad_reduce,
                                grad_comm_dtype=args.grad_comm_dtype,
-                               fsdp_wrap=args.fsdp_wrap)
+                               fsdp_wrap=args.fsdp_wrap, fsdp_sharding=args.fsdp_sharding)
         engine, ecfg = _engine_for(h, model, device)
         ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
         batches = make_batcher("device", ds, args.per_device_batch, eworld, engine.comm.rank, args.strategy, device)
@@ -303,6 +306,8 @@ def run_rank(args) -> int:
             label = "zero1"                  # window-reduced: ZeRO-1 communication
         if args.strategy == "fsdp" and ecfg.wrap == "root":
             label = "fsdp_root"
+        if args.strategy == "fsdp" and not ecfg.reshard_after_forward:
+            label += "_sgo"                  # shard_grad_op: no re-gather in backward
         if rank == 0:
             world = eworld if args.emulate else world
             flops = mcfg.train_flops_per_token(args.seq_len)

@@ -122,6 +122,8 @@ def _engine_for(args, model, device):
             fc = load_fsdp_config(path)
         if getattr(args, "fsdp_wrap", None) == "root":      # the reference's single root FlatParameter
             fc = dict(fc or {}, auto_wrap_policy="size_based")
+        if getattr(args, "fsdp_sharding", None):            # bench.py --fsdp-sharding (FSDP sharding_strategy)
+            fc = dict(fc or {}, sharding_strategy=args.fsdp_sharding)
     cfg = engine_config(args.strategy, args.grad_accum, args.accum_semantics, ds, fc,
                         compute_dtype=DTYPES[args.dtype], bucket_mb=args.bucket_mb, seed=args.seed,
                         grad_reduce=getattr(args, "grad_reduce", "micro"))

@@ -33,6 +33,10 @@ STRATS = {
     # BASELINE configs #2 / #3 name DDP and FSDP full-shard in bf16
     "ddp_bf16": ["--strategy", "ddp", "--dtype", "bf16"],
     "fsdp_bf16": ["--strategy", "fsdp", "--dtype", "bf16"],
+    # FSDP SHARD_GRAD_OP (configs/fsdp/fsdp_config.yaml's alternative, SURVEY §7.4 phase 3): the parameters
+    # gathered for the forward stay until the backward, so the backward re-gathers nothing (288 GB holds them)
+    "fsdp_sgo": ["--strategy", "fsdp", "--fsdp-sharding", "shard_grad_op"],
+    "fsdp_bf16_sgo": ["--strategy", "fsdp", "--dtype", "bf16", "--fsdp-sharding", "shard_grad_op"],
 }
 
 
