@@ -249,6 +249,180 @@ __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Direct-operand variant: the four waves split ONE operand's rows (PA: A / M, else B / N), so each wave's
+// rows of that operand are private -- they are loaded straight into MFMA fragments (16 rows x 64
+// contiguous bytes per load instruction, natural 16x16x32 k order), with no LDS round trip; only the
+// other operand, which all four waves read, is staged through LDS.  Per 64-deep k-step of a 128 x 64 tile
+// with A direct: 8 KB of ds_write and 32 KB of ds_read instead of 24 + 48 KB, and 8 ds_read_b128 per wave
+// instead of 12.  DP stages of private fragments and DS stages of the shared operand are in flight.
+template <int BM, int BN, bool PA, int DP, int DS>
+struct RsdGeo {
+  static constexpr int P_ROWS = PA ? BM : BN, S_ROWS = PA ? BN : BM;
+  static constexpr int PW = P_ROWS / 4;                 // private rows per wave
+  static constexpr int FP = PW / 16, FS = S_ROWS / 16;   // 16x16 MFMA tiles per wave along P / S
+  static constexpr int NS = S_ROWS / 32;                 // 16-byte pieces per thread per stage (shared operand)
+  static constexpr int STAGE = S_ROWS * 128;
+  static constexpr int U = (DP > DS ? DP : DS) < 2 ? 2 : (DP > DS ? DP : DS);   // DP, DS in {1, 2, 4}
+  static_assert(PW % 16 == 0 && S_ROWS % 32 == 0 && U % DP == 0 && U % DS == 0 && U % 2 == 0, "geometry");
+};
+
+template <int BM, int BN, bool PA, int DP, int DS>
+__global__ __launch_bounds__(256, 1) void gemm_rsd_kernel(RsArgs g) {
+  using G = RsdGeo<BM, BN, PA, DP, DS>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  int mb, nb;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {
+    const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  } else {
+    mb = idx / tiles_n;
+    nb = idx - mb * tiles_n;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = g.K / 64;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * 64 == g.K && nk % G::U == 0);
+
+  const long pld = PA ? g.lda : g.ldb, sld = PA ? g.ldb : g.lda;
+  const char* pbase = PA ? (const char*)(g.a + (long)m0 * g.lda) : (const char*)(g.b + (long)n0 * g.ldb);
+  const char* sbase = PA ? (const char*)(g.b + (long)n0 * g.ldb) : (const char*)(g.a + (long)m0 * g.lda);
+  const int fr = lane & 15, fq = lane >> 4;
+  // private fragment i of a wave: rows wave * PW + 16 i + fr, bytes 64 kk + 16 fq of the stage's 128
+  uint32_t vp[G::FP];
+#pragma unroll
+  for (int i = 0; i < G::FP; ++i) vp[i] = (uint32_t)(((wave * G::PW + 16 * i + fr) * pld) * 2 + 16 * fq);
+  // shared operand staging: piece i of a thread = row 32 i + tid / 8, chunk tid % 8
+  const int prow = tid >> 3, pch = tid & 7;
+  uint32_t vs[G::NS];
+#pragma unroll
+  for (int i = 0; i < G::NS; ++i) vs[i] = (uint32_t)(((32 * i + prow) * sld + pch * 8) * 2);
+  const uint32_t wlane = rs_off(prow, pch);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  uint32_t foff[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) foff[kk] = rs_off(fr, 4 * kk + fq);
+
+  struct PFrag {
+    rs_frag f[G::FP][2];
+  };
+  PFrag PR[DP];
+  u32x4 R[DS][G::NS];
+  auto pload = [&](int kt, PFrag& d) {
+    const char* pp = pbase + min(kt, nk - 1) * 128;
+#pragma unroll
+    for (int i = 0; i < G::FP; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        d.f[i][kk] = __builtin_bit_cast(rs_frag, *reinterpret_cast<const u32x4*>(pp + vp[i] + 64 * kk));
+  };
+  auto sload = [&](int kt, u32x4 (&r)[G::NS]) {
+    const char* ps = sbase + min(kt, nk - 1) * 128;
+#pragma unroll
+    for (int i = 0; i < G::NS; ++i) r[i] = *reinterpret_cast<const u32x4*>(ps + vs[i]);
+  };
+  auto swrite = [&](int buf, const u32x4 (&r)[G::NS]) {
+    const uint32_t base = lds0 + buf * G::STAGE + wlane;
+#pragma unroll
+    for (int i = 0; i < G::NS; ++i) *(lds_u4t*)(size_t)(base + 4096 * i) = r[i];
+  };
+  struct SFrag {
+    rs_frag f[G::FS];
+  };
+  auto fread = [&](SFrag& x, int buf, int kk) {
+    const uint32_t base = lds0 + buf * G::STAGE + foff[kk];
+#pragma unroll
+    for (int j = 0; j < G::FS; ++j) x.f[j] = __builtin_bit_cast(rs_frag, *(lds_u4t*)(size_t)(base + 16 * j * 128));
+  };
+  f32x4 acc[G::FP][G::FS];
+#pragma unroll
+  for (int i = 0; i < G::FP; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FS; ++j) acc[i][j] = f32x4{};
+  // MFMA(B fragment, A fragment): lane -> m, registers -> 4 consecutive n
+  auto mma = [&](const PFrag& p, int kk, const SFrag& x) {
+#pragma unroll
+    for (int i = 0; i < G::FP; ++i)
+#pragma unroll
+      for (int j = 0; j < G::FS; ++j) {
+        if constexpr (PA) acc[i][j] = mfma16(x.f[j], p.f[i][kk], acc[i][j]);
+        else acc[i][j] = mfma16(p.f[i][kk], x.f[j], acc[i][j]);
+      }
+  };
+
+  SFrag X, Y;
+#pragma unroll
+  for (int d = 0; d < DP; ++d) pload(d, PR[d]);
+#pragma unroll
+  for (int d = 0; d < DS; ++d) sload(d, R[d]);
+  swrite(0, R[0]);
+  sload(DS, R[0]);
+  __syncthreads();
+  fread(X, 0, 0);
+  swrite(1, R[1 % DS]);
+  sload(DS + 1, R[1 % DS]);
+  fread(Y, 0, 1);
+  __syncthreads();
+  for (int t = 0; t < nk; t += G::U) {
+#pragma unroll
+    for (int u = 0; u < G::U; ++u) {
+      const int kt = t + u;
+      mma(PR[u % DP], 0, X);
+      fread(X, (u + 1) & 1, 0);
+      swrite(u & 1, R[(u + 2) % DS]);
+      sload(kt + 2 + DS, R[(u + 2) % DS]);
+      mma(PR[u % DP], 1, Y);
+      fread(Y, (u + 1) & 1, 1);
+      pload(kt + DP, PR[u % DP]);
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < G::FP; ++i) {
+#pragma unroll
+    for (int j = 0; j < G::FS; ++j) {
+      const int m = PA ? m0 + wave * G::PW + 16 * i + fr : m0 + 16 * j + fr;
+      const int n = PA ? n0 + 16 * j + 4 * fq : n0 + wave * G::PW + 16 * i + 4 * fq;
+      bf16_t* cp = g.c + (size_t)m * g.ldc + n;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.bias) {
+        const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
+        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+      }
+      if (g.accumulate) {
+        const uint2 old = *reinterpret_cast<const uint2*>(cp);
+        v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+      }
+      uint2 o;
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(cp) = o;
+    }
+  }
+}
+
+template <int BM, int BN, bool PA, int DP, int DS>
+void launch_rsd(const RsArgs& g, hipStream_t st) {
+  constexpr int smem = 2 * RsdGeo<BM, BN, PA, DP, DS>::STAGE;
+  static_assert(smem <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_rsd_kernel<BM, BN, PA, DP, DS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_rsd_kernel<BM, BN, PA, DP, DS>), dim3(tiles), dim3(256), smem, st, g);
+}
+
 template <int BM, int BN, int WGM, int D, bool M32>
 void launch_rs(const RsArgs& g, hipStream_t st) {
   constexpr int smem = 2 * RsGeo<BM, BN, WGM, D, M32>::STAGE;
@@ -266,11 +440,17 @@ void launch_rs(const RsArgs& g, hipStream_t st) {
 struct RsCfg {
   int bm, bn, wgm, d;
   bool m32;
+  int dp = 0;        // > 0: direct-operand kernel, DP stages of private fragments (d = shared stages)
+  bool pa = false;   // direct kernel: A private (waves split M), else B private (waves split N)
 };
-// 0-2: N = 1024 products (16 x 16 tiles of 128 x 64); 3-4 / 6: N = 4096 (128 x 256); 5: N = 3072 (128 x 192)
+// 0-2: N = 1024 products (16 x 16 tiles of 128 x 64); 3-4 / 6: N = 4096 (128 x 256); 5: N = 3072 (128 x 192);
+// 8-12: direct-operand kernels
 constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {128, 64, 2, 2, true},
                              {128, 256, 2, 2, false}, {128, 256, 2, 2, true}, {128, 192, 2, 2, false},
-                             {128, 128, 2, 2, false}, {64, 128, 2, 2, false}};
+                             {128, 128, 2, 2, false}, {64, 128, 2, 2, false},
+                             {128, 64, 4, 2, false, 2, true}, {128, 64, 4, 2, false, 4, true},
+                             {128, 256, 1, 2, false, 2, false}, {128, 192, 1, 2, false, 2, false},
+                             {128, 128, 4, 2, false, 2, true}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -282,7 +462,12 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 4: launch_rs<128, 256, 2, 2, true>(g, st); break;
     case 5: launch_rs<128, 192, 2, 2, false>(g, st); break;
     case 6: launch_rs<128, 128, 2, 2, false>(g, st); break;
-    default: launch_rs<64, 128, 2, 2, false>(g, st); break;
+    case 7: launch_rs<64, 128, 2, 2, false>(g, st); break;
+    case 8: launch_rsd<128, 64, true, 2, 2>(g, st); break;
+    case 9: launch_rsd<128, 64, true, 4, 2>(g, st); break;
+    case 10: launch_rsd<128, 256, false, 2, 2>(g, st); break;
+    case 11: launch_rsd<128, 192, false, 2, 2>(g, st); break;
+    default: launch_rsd<128, 128, true, 2, 2>(g, st); break;
   }
 }
 
@@ -291,7 +476,8 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
 static bool rs_fits(int c, int M, int N, int K) {
   if (c < 0 || c >= kRsNumCfgs) return false;
   const RsCfg t = kRsCfgs[c];
-  const int u = t.d % 2 == 0 ? t.d : 2 * t.d;
+  const int dm = t.dp > t.d ? t.dp : t.d;
+  const int u = t.dp > 0 ? (dm < 2 ? 2 : dm) : (t.d % 2 == 0 ? t.d : 2 * t.d);
   return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % 64 == 0 && (K / 64) % u == 0;
 }
 

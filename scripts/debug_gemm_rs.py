@@ -11,7 +11,7 @@ import dltb  # noqa: E402,F401
 from dltb.ops._ext import ext  # noqa: E402
 
 TILE = {0: (128, 64), 1: (128, 64), 2: (128, 64), 3: (128, 256), 4: (128, 256), 5: (128, 192), 6: (128, 128),
-        7: (64, 128)}
+        7: (64, 128), 8: (128, 64), 9: (128, 64), 10: (128, 256), 11: (128, 192), 12: (128, 128)}
 C = ext()
 torch.manual_seed(0)
 for (M, N, K) in [(2048, 1024, 1024), (2048, 3072, 1024), (6144, 1024, 1024), (2048, 2048, 1024),
@@ -19,7 +19,7 @@ for (M, N, K) in [(2048, 1024, 1024), (2048, 3072, 1024), (6144, 1024, 1024), (2
     x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
     ref = x.float() @ w.float().t()
-    for c in (0, 6, 7):
+    for c in (0, 6, 7, 8, 10, 12):
         if not C.gemm_rs_supported(M, N, K, c):
             continue
         bm, bn = TILE[c]
