@@ -283,8 +283,11 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
   if (causal) qb = nqb - 1 - qb;
 }
 
-template <int D>
-constexpr int fwd_ks() { return D == 64 ? DLTB_FWD_KS64 : 2; }   // KS = 4: 2-deep ring, 128 VGPRs
+// KS = 4: 2-deep ring, 128 VGPRs without scratch for the non-causal (TinyGPT) kernels; the causal D = 64
+// instantiations spill at 4 (16 / 28 B of scratch per lane without / with dropout) and run at 3 (151-152
+// VGPRs, no scratch): profiles/attention_d64_resources_r5.txt
+template <int D, bool C = false>
+constexpr int fwd_ks() { return D == 64 ? (C && DLTB_FWD_KS64 > 3 ? 3 : DLTB_FWD_KS64) : 2; }
 template <int D, int KS>
 constexpr int fwd_nst() {   // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
   return D == 64 && KS == 2 && DLTB_FWD_PP ? DLTB_FWD_PP_NST : (D == 64 && KS < 4 ? 3 : 2);
@@ -898,16 +901,17 @@ __global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restric
 
 // =============================================================================== dQ
 // Query-major, KS key-splits per workgroup as in the forward; dQ partials merge through LDS.
-template <int D>
-constexpr int dq_ks() { return D == 64 ? DLTB_DQ_KS64 : 2; }
+// causal D = 64 with dropout spills at 3 (40 B of scratch per lane): 2 splits there (188 VGPRs, no scratch)
+template <int D, bool C = false>
+constexpr int dq_ks() { return D == 64 ? (C && DLTB_DQ_KS64 > 2 ? 2 : DLTB_DQ_KS64) : 2; }
 template <int D>
 constexpr int dq_nst() { return D == 64 ? 3 : 2; }   // LDS ring depth, as the forward's
 template <int D>
 constexpr int dq_stage_bytes() { return 2 * kTile * D * 2 + 1024; }   // K, V, dropout words of 4 waves
-template <int D>
+template <int D, int KS = dq_ks<D>()>
 constexpr int dq_smem_bytes() {
-  constexpr int ring = dq_nst<D>() * dq_ks<D>() * dq_stage_bytes<D>();
-  constexpr int merge = (dq_ks<D>() - 1) * 4 * 16 * (D / 32) * 64 * 4;
+  constexpr int ring = dq_nst<D>() * KS * dq_stage_bytes<D>();
+  constexpr int merge = (KS - 1) * 4 * 16 * (D / 32) * 64 * 4;
   return ring > merge ? ring : merge;
 }
 
@@ -1070,7 +1074,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
   __syncthreads();              // all LDS reads done before the ring is reused for the merge
   if constexpr (KS > 1) {      // splits 1..KS-1 -> LDS -> split 0
     constexpr int NF = 16 * NACC;
-    static_assert((KS - 1) * 4 * NF * 64 * 4 <= dq_smem_bytes<D>(), "merge buffer exceeds the LDS ring");
+    static_assert((KS - 1) * 4 * NF * 64 * 4 <= dq_smem_bytes<D, KS>(), "merge buffer exceeds the LDS ring");
     float* red0 = reinterpret_cast<float*>(smem) + qw * NF * 64 + lane;
     if (sp > 0) {
       float* red = red0 + (sp - 1) * 4 * NF * 64;
@@ -1126,19 +1130,20 @@ namespace {
 
 template <int D, bool C, bool DR>
 void set_attrs() {
-  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, C, DR, fwd_ks<D>()>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, fwd_smem_bytes<D>());
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR, dq_ks<D>()>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, dq_smem_bytes<D>());
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, C, DR, fwd_ks<D, C>()>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, fwd_smem_bytes<D, fwd_ks<D, C>()>());
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR, dq_ks<D, C>()>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, dq_smem_bytes<D, dq_ks<D, C>()>());
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, C, DR, dkdv_ks<D>()>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, dkdv_smem_bytes<D>());
 }
 
 template <int D, bool C, bool DR>
 void launch_fwd(const AttnArgs& a, hipStream_t st) {
-  constexpr int KS = fwd_ks<D>();
+  constexpr int KS = fwd_ks<D, C>();
+  constexpr int smem = fwd_smem_bytes<D, KS>();
   dim3 grid((a.T / kBlockRows) * a.B * a.Hq);
-  hipLaunchKernelGGL((attn_fwd_kernel<D, C, DR, KS>), grid, dim3(256 * KS), fwd_smem_bytes<D>(), st, a);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, C, DR, KS>), grid, dim3(256 * KS), smem, st, a);
 }
 
 #define DLTB_ATTN_DISPATCH(FN, D, C, DR, ...)           \
@@ -1220,9 +1225,10 @@ void launch_dkdv(const AttnArgs& a, hipStream_t st) {
 }
 template <int D, bool C, bool DR>
 void launch_dq(const AttnArgs& a, hipStream_t st) {
-  constexpr int KS = dq_ks<D>();
+  constexpr int KS = dq_ks<D, C>();
+  constexpr int smem = dq_smem_bytes<D, KS>();
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hq), dim3(256 * KS),
-                     dq_smem_bytes<D>(), st, a);
+                     smem, st, a);
 }
 }  // namespace
 
