@@ -388,6 +388,17 @@ def run_rank(args) -> int:
                     "emu_channels": engine.comm.emu_channels,
                     "emu_hbm_passes": engine.comm.emu_pass_of,
                     "emu_host_us_per_call": engine.comm.emu_host_us,
+                    # what of the model is measured and what is assumed (no N-GPU RCCL run backs the latter)
+                    "emu_assumptions": {
+                        "hbm_passes": "ASSUMED: ring-algorithm estimate (reduce-scatter 3, all-gather 2, all-reduce 5 "
+                                      "passes over the buffer), not measured on RCCL",
+                        "channels": f"ASSUMED: {engine.comm.emu_channels}-workgroup stand-in for RCCL's CU footprint",
+                        "host_us": "MEASURED: 1-rank RCCL communicator, async calls with the GPU held busy "
+                                   "(profiles/pg_host_cost.json); the sync scalar norm all-reduce has its own 9.7 us row"
+                                   if engine.comm.emu_host_us else "none (no host-cost profile)",
+                        "alpha_beta": {op: src for op, (a, b, src) in engine.comm.emu_params.items()
+                                       if op in ("all_reduce", "reduce_scatter", "all_gather")},
+                    },
                     "comm_model_ms_per_step": comm_model_ms,
                     "vs_baseline": None, "vs_baseline_per_gpu": None,
                     "predicted_ms_per_step": ms,

@@ -252,6 +252,8 @@ class Comm:
         side.wait_stream(torch.cuda.current_stream(full.device))   # starts after its producers
         alpha, beta = self._emu_time(op, full)
         host = self.emu_host_us.get(op, 0.0)
+        if op == "all_reduce" and not async_op and full.numel() <= 16 and "all_reduce_scalar_sync" in self.emu_host_us:
+            host = self.emu_host_us["all_reduce_scalar_sync"]   # the clip norm's own measured (sync, 1 float) cost
         if host > 0:                          # the ProcessGroupNCCL call's host time
             t_end = time.perf_counter() + host * 1e-6
             while time.perf_counter() < t_end:
