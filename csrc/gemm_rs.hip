@@ -79,10 +79,22 @@ struct RsGeo {
   static_assert(WM % T == 0 && WN % T == 0 && BM % 32 == 0 && BN % 32 == 0, "tile shape");
 };
 
+// Workgroup barrier that no LDS access can cross in either direction.  __syncthreads() alone is not a
+// compiler barrier for these accesses: hipcc (ROCm 7.2) sank a fragment read of the buffer that the
+// next k-step overwrites below the barrier that was to order it -- other waves' writes then raced it
+// (wrong tiles whenever waves drifted apart, e.g. with 2-3 workgroups per CU; scripts/debug_gemm_rs.py).
+DLTB_DEV void rs_barrier() {
+  asm volatile("" ::: "memory");
+  __syncthreads();
+  asm volatile("" ::: "memory");
+}
+
+DLTB_DEV void wait_vm0() { __builtin_amdgcn_s_waitcnt((0) | (0 << 14) | (7 << 4) | (15 << 8)); }
+
 // byte offset of 16-byte chunk `ch` of row `row` in a [rows][64] bf16 LDS image
 DLTB_DEV uint32_t rs_off(int row, int ch) { return (uint32_t)(row * 128 + ((ch ^ ((row >> 1) & 7)) << 4)); }
 
-template <int BM, int BN, int WGM, int D, bool M32>
+template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
 __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
   using G = RsGeo<BM, BN, WGM, D, M32>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -175,6 +187,16 @@ __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
     }
   };
   auto mma = [&](const Frags& f) {
+    if constexpr ((DBG & 8) != 0) {          // ablation: operands kept live, no MFMA
+#pragma unroll
+      for (int s = 0; s < KH; ++s) {
+#pragma unroll
+        for (int i = 0; i < G::FM; ++i) asm volatile("" ::"v"(f.a[s][i]));
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) asm volatile("" ::"v"(f.b[s][j]));
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < KH; ++s)
 #pragma unroll
@@ -192,12 +214,12 @@ __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
   for (int d = 0; d < D; ++d) gload(d, R[d]);
   swrite(0, R[0]);
   gload(D, R[0]);
-  __syncthreads();                                   // stage 0 visible
+  rs_barrier();                                      // stage 0 visible
   fread(X, 0, 0);
   swrite(1, R[1 % D]);
   gload(D + 1, R[1 % D]);
   fread(Y, 0, 1);
-  __syncthreads();                                   // stage 1 visible, stage 0's reads drained
+  rs_barrier();                                      // stage 1 visible, stage 0's reads drained
 
   // ---- main loop.  Top of k-step kt: X / Y hold stage kt's fragments, stage kt + 1 is visible in
   // buffer (kt + 1) & 1 and buffer kt & 1 is free (every wave drained its reads of stage kt before
@@ -210,15 +232,20 @@ __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
 #pragma unroll
     for (int u = 0; u < G::U; ++u) {
       const int kt = t + u;
-      mma(X);
-      fread(X, (u + 1) & 1, 0);
-      swrite(u & 1, R[(u + 2) % D]);
-      gload(kt + 2 + D, R[(u + 2) % D]);
-      mma(Y);
-      fread(Y, (u + 1) & 1, 1);
-      __syncthreads();
+      // (DBG & 16 / 32 / 64: ablation builds without the loop's global loads / fragment reads and
+      // MFMAs / LDS writes -- timing only)
+      if constexpr ((DBG & 32) == 0) mma(X);
+      if constexpr ((DBG & 4) != 0) rs_barrier();
+      if constexpr ((DBG & 32) == 0) fread(X, (u + 1) & 1, 0);
+      if constexpr ((DBG & 64) == 0) swrite(u & 1, R[(u + 2) % D]);
+      if constexpr ((DBG & 16) == 0) gload(kt + 2 + D, R[(u + 2) % D]);
+      if constexpr ((DBG & 32) == 0) mma(Y);
+      if constexpr ((DBG & 4) != 0) rs_barrier();
+      if constexpr ((DBG & 32) == 0) fread(Y, (u + 1) & 1, 1);
+      rs_barrier();
     }
   }
+  if constexpr ((DBG & 1) != 0) wait_vm0();
 
   // ---- epilogue: lane -> row m, 4 consecutive columns per register group
 #pragma unroll
@@ -364,12 +391,12 @@ __global__ __launch_bounds__(256, 1) void gemm_rsd_kernel(RsArgs g) {
   for (int d = 0; d < DS; ++d) sload(d, R[d]);
   swrite(0, R[0]);
   sload(DS, R[0]);
-  __syncthreads();
+  rs_barrier();
   fread(X, 0, 0);
   swrite(1, R[1 % DS]);
   sload(DS + 1, R[1 % DS]);
   fread(Y, 0, 1);
-  __syncthreads();
+  rs_barrier();
   for (int t = 0; t < nk; t += G::U) {
 #pragma unroll
     for (int u = 0; u < G::U; ++u) {
@@ -381,7 +408,7 @@ __global__ __launch_bounds__(256, 1) void gemm_rsd_kernel(RsArgs g) {
       mma(PR[u % DP], 1, Y);
       fread(Y, (u + 1) & 1, 1);
       pload(kt + DP, PR[u % DP]);
-      __syncthreads();
+      rs_barrier();
     }
   }
 
@@ -423,18 +450,19 @@ void launch_rsd(const RsArgs& g, hipStream_t st) {
   hipLaunchKernelGGL((gemm_rsd_kernel<BM, BN, PA, DP, DS>), dim3(tiles), dim3(256), smem, st, g);
 }
 
-template <int BM, int BN, int WGM, int D, bool M32>
+template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
 void launch_rs(const RsArgs& g, hipStream_t st) {
-  constexpr int smem = 2 * RsGeo<BM, BN, WGM, D, M32>::STAGE;
+  // (DBG & 2: debug builds pad the LDS to 100 KB: one workgroup per CU)
+  constexpr int smem = 2 * RsGeo<BM, BN, WGM, D, M32>::STAGE + ((DBG & 2) ? 102400 : 0);
   static_assert(smem <= 163840, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_rs_kernel<BM, BN, WGM, D, M32>,
+    (void)hipFuncSetAttribute((const void*)gemm_rs_kernel<BM, BN, WGM, D, M32, DBG>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int tiles = (g.M / BM) * (g.N / BN);
-  hipLaunchKernelGGL((gemm_rs_kernel<BM, BN, WGM, D, M32>), dim3(tiles), dim3(256), smem, st, g);
+  hipLaunchKernelGGL((gemm_rs_kernel<BM, BN, WGM, D, M32, DBG>), dim3(tiles), dim3(256), smem, st, g);
 }
 
 struct RsCfg {
@@ -450,7 +478,15 @@ constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {12
                              {128, 128, 2, 2, false}, {64, 128, 2, 2, false},
                              {128, 64, 4, 2, false, 2, true}, {128, 64, 4, 2, false, 4, true},
                              {128, 256, 1, 2, false, 2, false}, {128, 192, 1, 2, false, 2, false},
-                             {128, 128, 4, 2, false, 2, true}};
+                             {128, 128, 4, 2, false, 2, true},
+                             // 13-15: debug variants of cfg 0 (vmcnt(0) before the epilogue / one workgroup
+                             // per CU / a barrier after every MFMA half)
+                             {128, 64, 2, 2, false}, {128, 64, 2, 2, false}, {128, 64, 2, 2, false},
+                             // 16-19 / 20-23: ablations of cfg 4 / cfg 1 (no MFMA / no loop loads / no
+                             // fragment reads + MFMA / no LDS writes): timing only
+                             {128, 256, 2, 2, true}, {128, 256, 2, 2, true}, {128, 256, 2, 2, true},
+                             {128, 256, 2, 2, true}, {128, 64, 2, 4, false}, {128, 64, 2, 4, false},
+                             {128, 64, 2, 4, false}, {128, 64, 2, 4, false}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -467,7 +503,18 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 9: launch_rsd<128, 64, true, 4, 2>(g, st); break;
     case 10: launch_rsd<128, 256, false, 2, 2>(g, st); break;
     case 11: launch_rsd<128, 192, false, 2, 2>(g, st); break;
-    default: launch_rsd<128, 128, true, 2, 2>(g, st); break;
+    case 12: launch_rsd<128, 128, true, 2, 2>(g, st); break;
+    case 13: launch_rs<128, 64, 2, 2, false, 1>(g, st); break;
+    case 14: launch_rs<128, 64, 2, 2, false, 2>(g, st); break;
+    case 15: launch_rs<128, 64, 2, 2, false, 4>(g, st); break;
+    case 16: launch_rs<128, 256, 2, 2, true, 8>(g, st); break;
+    case 17: launch_rs<128, 256, 2, 2, true, 16>(g, st); break;
+    case 18: launch_rs<128, 256, 2, 2, true, 32>(g, st); break;
+    case 19: launch_rs<128, 256, 2, 2, true, 64>(g, st); break;
+    case 20: launch_rs<128, 64, 2, 4, false, 8>(g, st); break;
+    case 21: launch_rs<128, 64, 2, 4, false, 16>(g, st); break;
+    case 22: launch_rs<128, 64, 2, 4, false, 32>(g, st); break;
+    default: launch_rs<128, 64, 2, 4, false, 64>(g, st); break;
   }
 }
 
