@@ -62,6 +62,45 @@ DLTB_DEV f32x16 mfma32(rs_frag a, rs_frag b, f32x16 c) {
 #endif
 }
 
+// Coalesced epilogue through LDS (the stage buffers are free after the k-loop's last barrier).  An MFMA
+// accumulator gives each lane 4 consecutive columns of ONE row, so storing it directly is a row-per-lane
+// store: every 8-byte store instruction touches 64 rows (cache lines) -- store-issue bound, ~2-9 us at the
+// end of every product.  Phase 1: each lane adds the bias in fp32, rounds once to bf16 and writes its
+// 8-byte pieces into a [BM][BN + 8] image (16-byte aligned rows, b64 writes conflict-free); phase 2: 16-byte
+// chunks, 8 lanes per 128-byte row segment, to global memory (accumulate adds the old C there, in fp32).
+template <int BM, int BN>
+struct RsEpi {
+  static constexpr int P = BN + 8;                 // row pitch (elements)
+  static constexpr int BYTES = BM * P * 2;
+  DLTB_DEV static void put(uint32_t lds0, const bf16_t* bias, int n0, int ml, int nl, const float* a) {
+    float v[4] = {a[0], a[1], a[2], a[3]};
+    if (bias) {
+      const uint2 bb = *reinterpret_cast<const uint2*>(bias + n0 + nl);
+      v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+    }
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+    *(__attribute__((address_space(3))) u32x2*)(size_t)(lds0 + (ml * P + nl) * 2) = o;
+  }
+  DLTB_DEV static void flush(const RsArgs& g, uint32_t lds0, int m0, int n0, int tid) {
+    constexpr int CPR = BN / 8, CHUNKS = BM * CPR;
+    static_assert(CHUNKS % 256 == 0, "epilogue chunks");
+#pragma unroll 4
+    for (int c = tid; c < CHUNKS; c += 256) {
+      const int row = c / CPR, ch = c - row * CPR;
+      u32x4 v = *(lds_u4t*)(size_t)(lds0 + (row * P + ch * 8) * 2);
+      bf16_t* dst = g.c + (size_t)(m0 + row) * g.ldc + n0 + ch * 8;
+      if (g.accumulate) {
+        const u32x4 old = *reinterpret_cast<const u32x4*>(dst);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = pack_bf2(lo_bf(v[e]) + lo_bf(old[e]), hi_bf(v[e]) + hi_bf(old[e]));
+      }
+      *reinterpret_cast<u32x4*>(dst) = v;
+    }
+  }
+};
+
 template <int BM, int BN, int WGM, int D, bool M32>
 struct RsGeo {
   static_assert(4 % WGM == 0, "4 waves");
@@ -87,6 +126,12 @@ DLTB_DEV void rs_barrier() {
   asm volatile("" ::: "memory");
   __syncthreads();
   asm volatile("" ::: "memory");
+}
+
+DLTB_DEV uint32_t lane_addr(uint32_t sbase, uint32_t off) {
+  uint32_t a;
+  asm("v_add_u32 %0, %1, %2" : "=v"(a) : "s"(sbase), "v"(off));
+  return a;
 }
 
 DLTB_DEV void wait_vm0() { __builtin_amdgcn_s_waitcnt((0) | (0 << 14) | (7 << 4) | (15 << 8)); }
@@ -247,33 +292,219 @@ __global__ __launch_bounds__(256, 1) void gemm_rs_kernel(RsArgs g) {
   }
   if constexpr ((DBG & 1) != 0) wait_vm0();
 
-  // ---- epilogue: lane -> row m, 4 consecutive columns per register group
+  // ---- epilogue: lane -> row m, 4 consecutive columns per register group, through LDS
+  using E = RsEpi<BM, BN>;
+  static_assert(E::BYTES <= 2 * G::STAGE, "epilogue image exceeds the stage buffers");
 #pragma unroll
   for (int i = 0; i < G::FM; ++i) {
-    const int m = m0 + arow0 + G::T * i + fr;
-    bf16_t* crow = g.c + (size_t)m * g.ldc;
 #pragma unroll
     for (int j = 0; j < G::FN; ++j) {
 #pragma unroll
       for (int q = 0; q < G::ACC / 4; ++q) {
         // 16x16: columns 4 fq .. +3;  32x32: register group q -> columns 8 q + 4 fq .. +3
-        const int n = n0 + brow0 + G::T * j + (M32 ? 8 * q + 4 * fq : 4 * fq);
-        float v[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        if (g.bias) {
-          const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
-          v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
-        }
-        if (g.accumulate) {
-          const uint2 old = *reinterpret_cast<const uint2*>(crow + n);
-          v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
-        }
-        uint2 o;
-        o.x = pack_bf2(v[0], v[1]);
-        o.y = pack_bf2(v[2], v[3]);
-        *reinterpret_cast<uint2*>(crow + n) = o;
+        const float a4[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        E::put(lds0, g.bias, n0, arow0 + G::T * i + fr, brow0 + G::T * j + (M32 ? 8 * q + 4 * fq : 4 * fq), a4);
       }
     }
   }
+  rs_barrier();
+  E::flush(g, lds0, m0, n0, tid);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Software-pipelined variant (round 5, the step's kernel): three LDS buffers and an explicit instruction
+// interleave.  hipcc emits a k-step's MFMAs as one back-to-back cluster; a wave alone on its SIMD issues in
+// order, so the LDS reads, LDS writes and global loads queued behind that cluster only start when its last
+// MFMA has issued, and the MFMA pipe then idles while they drain (ablation: MFMA time and memory time
+// ADD UP -- cfg 16-25).  Here each k-step is two halves and every MFMA of a half is followed by its share
+// of the memory instructions (__builtin_amdgcn_sched_group_barrier), so they issue in the MFMA shadows:
+//   segment kt (stage s lives in LDS buffer s % 3):
+//     MFMAs of half 0 (X)  ||  read half 1 of stage kt into Y, write stage kt + 2, load stage kt + 2 + D
+//     MFMAs of half 1 (Y)  ||  read half 0 of stage kt + 1 into X
+//     one barrier
+// Buffer (kt + 2) % 3 held stage kt - 1, whose last reads were issued before the previous barrier; the
+// reads of stage kt / kt + 1 are of stages written two / one segments earlier.  Global loads are buffer
+// loads (the k offset in the SGPR soffset: no per-load address VALU).
+template <int N>
+struct RsInt {
+  // distribute T items over N slots: the count of slot k
+  static constexpr int share(int T, int k) { return (T * (k + 1)) / N - (T * k) / N; }
+};
+template <int NM, int NR, int NW, int NL, int K = 0>
+DLTB_DEV void rs_interleave() {
+  if constexpr (K < NM) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                           // one MFMA
+    constexpr int r = RsInt<NM>::share(NR, K), w = RsInt<NM>::share(NW, K), l = RsInt<NM>::share(NL, K);
+    if constexpr (r > 0) __builtin_amdgcn_sched_group_barrier(0x100, r, 0);       // DS reads
+    if constexpr (w > 0) __builtin_amdgcn_sched_group_barrier(0x200, w, 0);       // DS writes
+    if constexpr (l > 0) __builtin_amdgcn_sched_group_barrier(0x020, l, 0);       // VMEM reads
+    rs_interleave<NM, NR, NW, NL, K + 1>();
+  }
+}
+
+template <int BM, int BN, int WGM, int D, bool M32>
+__global__ __launch_bounds__(256, 1) void gemm_rsp_kernel(RsArgs g) {
+  using G = RsGeo<BM, BN, WGM, D, M32>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WGM, wn = wave / WGM;
+
+  const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  int mb, nb;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {
+    const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  } else {
+    mb = idx / tiles_n;
+    nb = idx - mb * tiles_n;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = g.K / G::BK;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * G::BK == g.K && nk % D == 0 && nk >= 2);
+
+  const int prow = tid >> 3, pch = tid & 7;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.a + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.b + (long)n0 * g.ldb), (short)0, 0x7fffffff, 0x00020000);
+  uint32_t voa[G::NA], vob[G::NB];
+#pragma unroll
+  for (int i = 0; i < G::NA; ++i) voa[i] = (uint32_t)(((32 * i + prow) * g.lda + pch * 8) * 2);
+#pragma unroll
+  for (int i = 0; i < G::NB; ++i) vob[i] = (uint32_t)(((32 * i + prow) * g.ldb + pch * 8) * 2);
+  const uint32_t wlane = rs_off(prow, pch);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+
+  u32x4 R[D][G::NI];
+  auto gload = [&](int kt, u32x4 (&r)[G::NI]) {
+    const int so = min(kt, nk - 1) * (G::BK * 2);   // past the end: the last stage again (never consumed)
+#pragma unroll
+    for (int i = 0; i < G::NA; ++i) r[i] = __builtin_amdgcn_raw_buffer_load_b128(ra, voa[i], so, 0);
+#pragma unroll
+    for (int i = 0; i < G::NB; ++i) r[G::NA + i] = __builtin_amdgcn_raw_buffer_load_b128(rb, vob[i], so, 0);
+  };
+  auto swrite = [&](uint32_t bufbase, const u32x4 (&r)[G::NI]) {
+    const uint32_t base = bufbase + wlane;
+#pragma unroll
+    for (int i = 0; i < G::NA; ++i) *(lds_u4t*)(size_t)(base + 4096 * i) = r[i];
+#pragma unroll
+    for (int i = 0; i < G::NB; ++i) *(lds_u4t*)(size_t)(base + G::A_BYTES + 4096 * i) = r[G::NA + i];
+  };
+
+  constexpr int RL = M32 ? 32 : 16;
+  const int fr = lane & (RL - 1), fq = M32 ? (lane >> 5) : (lane >> 4);
+  const int arow0 = wm * G::WM, brow0 = wn * G::WN;
+  // per-lane fragment offsets with the wave's row base folded in: a fragment read is then one
+  // (buffer base + lane offset) add per k-substep and operand, the tile rows an immediate offset
+  uint32_t foa[G::KS], fob[G::KS];
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s) {
+    foa[s] = rs_off(fr, (M32 ? 2 : 4) * s + fq) + arow0 * 128;
+    fob[s] = rs_off(fr, (M32 ? 2 : 4) * s + fq) + G::A_BYTES + brow0 * 128;
+  }
+
+  using Acc = typename std::conditional<M32, f32x16, f32x4>::type;
+  Acc acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = Acc{};
+
+  constexpr int KH = G::KS / 2;
+  struct Frags {
+    rs_frag a[KH][G::FM], b[KH][G::FN];
+  };
+  auto fread = [&](Frags& f, uint32_t bufbase, int half) {
+#pragma unroll
+    for (int s = 0; s < KH; ++s) {
+      const uint32_t pa = lane_addr(bufbase, foa[half * KH + s]), pb = lane_addr(bufbase, fob[half * KH + s]);
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+        f.a[s][i] = __builtin_bit_cast(rs_frag, *(lds_u4t*)(size_t)(pa + G::T * i * 128));
+#pragma unroll
+      for (int j = 0; j < G::FN; ++j)
+        f.b[s][j] = __builtin_bit_cast(rs_frag, *(lds_u4t*)(size_t)(pb + G::T * j * 128));
+    }
+  };
+  auto mma = [&](const Frags& f) {
+#pragma unroll
+    for (int s = 0; s < KH; ++s)
+#pragma unroll
+      for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::FN; ++j) {
+          if constexpr (M32) acc[i][j] = mfma32(f.b[s][j], f.a[s][i], acc[i][j]);
+          else acc[i][j] = mfma16(f.b[s][j], f.a[s][i], acc[i][j]);
+        }
+  };
+  constexpr int NM = KH * G::FM * G::FN, NR = KH * (G::FM + G::FN);
+
+  // ---- prologue: stages 0 and 1 in buffers 0 / 1, half 0 of stage 0 in X
+  Frags X, Y;
+#pragma unroll
+  for (int d = 0; d < D; ++d) gload(d, R[d]);
+  swrite(lds0, R[0]);
+  gload(D, R[0]);
+  swrite(lds0 + G::STAGE, R[1 % D]);
+  gload(D + 1, R[1 % D]);
+  rs_barrier();
+  fread(X, lds0, 0);
+  uint32_t b_cur = lds0, b_nxt = lds0 + G::STAGE, b_wr = lds0 + 2 * G::STAGE;   // stage kt, kt + 1, kt + 2
+
+  for (int t = 0; t < nk; t += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int kt = t + u;
+      mma(X);
+      fread(Y, b_cur, 1);
+      swrite(b_wr, R[(u + 2) % D]);
+      gload(kt + 2 + D, R[(u + 2) % D]);
+      rs_interleave<NM, NR, G::NI, G::NI>();
+      mma(Y);
+      fread(X, b_nxt, 0);
+      rs_interleave<NM, NR, 0, 0>();
+      rs_barrier();
+      const uint32_t b_old = b_cur;
+      b_cur = b_nxt;
+      b_nxt = b_wr;
+      b_wr = b_old;
+    }
+  }
+
+  using E = RsEpi<BM, BN>;
+  static_assert(E::BYTES <= 3 * G::STAGE, "epilogue image exceeds the stage buffers");
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+#pragma unroll
+      for (int q = 0; q < G::ACC / 4; ++q) {
+        const float a4[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        E::put(lds0, g.bias, n0, arow0 + G::T * i + fr, brow0 + G::T * j + (M32 ? 8 * q + 4 * fq : 4 * fq), a4);
+      }
+    }
+  }
+  rs_barrier();
+  E::flush(g, lds0, m0, n0, tid);
+}
+
+template <int BM, int BN, int WGM, int D, bool M32>
+void launch_rsp(const RsArgs& g, hipStream_t st) {
+  constexpr int smem = 3 * RsGeo<BM, BN, WGM, D, M32>::STAGE;
+  static_assert(smem <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_rsp_kernel<BM, BN, WGM, D, M32>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_rsp_kernel<BM, BN, WGM, D, M32>), dim3(tiles), dim3(256), smem, st, g);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -412,33 +643,25 @@ __global__ __launch_bounds__(256, 1) void gemm_rsd_kernel(RsArgs g) {
     }
   }
 
+  using E = RsEpi<BM, BN>;
 #pragma unroll
   for (int i = 0; i < G::FP; ++i) {
 #pragma unroll
     for (int j = 0; j < G::FS; ++j) {
-      const int m = PA ? m0 + wave * G::PW + 16 * i + fr : m0 + 16 * j + fr;
-      const int n = PA ? n0 + 16 * j + 4 * fq : n0 + wave * G::PW + 16 * i + 4 * fq;
-      bf16_t* cp = g.c + (size_t)m * g.ldc + n;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (g.bias) {
-        const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n);
-        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
-      }
-      if (g.accumulate) {
-        const uint2 old = *reinterpret_cast<const uint2*>(cp);
-        v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
-      }
-      uint2 o;
-      o.x = pack_bf2(v[0], v[1]);
-      o.y = pack_bf2(v[2], v[3]);
-      *reinterpret_cast<uint2*>(cp) = o;
+      const int ml = PA ? wave * G::PW + 16 * i + fr : 16 * j + fr;
+      const int nl = PA ? 16 * j + 4 * fq : wave * G::PW + 16 * i + 4 * fq;
+      const float a4[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      E::put(lds0, g.bias, n0, ml, nl, a4);
     }
   }
+  rs_barrier();
+  E::flush(g, lds0, m0, n0, tid);
 }
 
 template <int BM, int BN, bool PA, int DP, int DS>
 void launch_rsd(const RsArgs& g, hipStream_t st) {
-  constexpr int smem = 2 * RsdGeo<BM, BN, PA, DP, DS>::STAGE;
+  constexpr int ring = 2 * RsdGeo<BM, BN, PA, DP, DS>::STAGE, epi = RsEpi<BM, BN>::BYTES;
+  constexpr int smem = ring > epi ? ring : epi;
   static_assert(smem <= 163840, "LDS budget");
   static bool attr = false;
   if (!attr) {
@@ -470,6 +693,7 @@ struct RsCfg {
   bool m32;
   int dp = 0;        // > 0: direct-operand kernel, DP stages of private fragments (d = shared stages)
   bool pa = false;   // direct kernel: A private (waves split M), else B private (waves split N)
+  int kind = 0;      // 2: software-pipelined kernel (3 LDS buffers)
 };
 // 0-2: N = 1024 products (16 x 16 tiles of 128 x 64); 3-4 / 6: N = 4096 (128 x 256); 5: N = 3072 (128 x 192);
 // 8-12: direct-operand kernels
@@ -486,7 +710,13 @@ constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {12
                              // fragment reads + MFMA / no LDS writes): timing only
                              {128, 256, 2, 2, true}, {128, 256, 2, 2, true}, {128, 256, 2, 2, true},
                              {128, 256, 2, 2, true}, {128, 64, 2, 4, false}, {128, 64, 2, 4, false},
-                             {128, 64, 2, 4, false}, {128, 64, 2, 4, false}};
+                             {128, 64, 2, 4, false}, {128, 64, 2, 4, false},
+                             // 24 / 25: cfg 4 / cfg 1 with an empty k-loop (launch + prologue + epilogue)
+                             {128, 256, 2, 2, true}, {128, 64, 2, 4, false},
+                             // 26-31: software-pipelined kernel (gemm_rsp_kernel; kind 2)
+                             {128, 64, 2, 2, false, 0, false, 2}, {128, 64, 2, 4, false, 0, false, 2},
+                             {128, 64, 2, 4, true, 0, false, 2}, {128, 256, 2, 2, true, 0, false, 2},
+                             {128, 192, 2, 2, false, 0, false, 2}, {128, 128, 2, 2, true, 0, false, 2}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -514,7 +744,15 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 20: launch_rs<128, 64, 2, 4, false, 8>(g, st); break;
     case 21: launch_rs<128, 64, 2, 4, false, 16>(g, st); break;
     case 22: launch_rs<128, 64, 2, 4, false, 32>(g, st); break;
-    default: launch_rs<128, 64, 2, 4, false, 64>(g, st); break;
+    case 23: launch_rs<128, 64, 2, 4, false, 64>(g, st); break;
+    case 24: launch_rs<128, 256, 2, 2, true, 112>(g, st); break;
+    case 25: launch_rs<128, 64, 2, 4, false, 112>(g, st); break;
+    case 26: launch_rsp<128, 64, 2, 2, false>(g, st); break;
+    case 27: launch_rsp<128, 64, 2, 4, false>(g, st); break;
+    case 28: launch_rsp<128, 64, 2, 4, true>(g, st); break;
+    case 29: launch_rsp<128, 256, 2, 2, true>(g, st); break;
+    case 30: launch_rsp<128, 192, 2, 2, false>(g, st); break;
+    default: launch_rsp<128, 128, 2, 2, true>(g, st); break;
   }
 }
 
@@ -524,7 +762,7 @@ static bool rs_fits(int c, int M, int N, int K) {
   if (c < 0 || c >= kRsNumCfgs) return false;
   const RsCfg t = kRsCfgs[c];
   const int dm = t.dp > t.d ? t.dp : t.d;
-  const int u = t.dp > 0 ? (dm < 2 ? 2 : dm) : (t.d % 2 == 0 ? t.d : 2 * t.d);
+  const int u = t.kind == 2 ? t.d : t.dp > 0 ? (dm < 2 ? 2 : dm) : (t.d % 2 == 0 ? t.d : 2 * t.d);
   return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % 64 == 0 && (K / 64) % u == 0;
 }
 
