@@ -361,6 +361,47 @@ def attn_bwd(q, k, v, o, do, lse, aux, dq, dk, dv, B, T, Hq, Hkv, scale, causal,
 
 
 # ------------------------------------------------------------------------------ linear
+# Own MFMA GEMM (csrc/gemm_rs.hip, register-staged, software-pipelined) for the per-layer NT products
+# C[M, N] = A[M, K] B[N, K]^T (+ bias) where it beats the tuned hipBLASLt solution: the shapes, tile
+# configs and tile walks come from configs/gemm_rs/gemm_rs_gfx950.csv (written by
+# scripts/tune_gemm_rs.py from same-process A/B timings); DLTB_OWN_GEMM=0 turns the dispatch off.
+import csv as _csv
+import os as _os
+
+_RS_FILE = _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))),
+                         "configs", "gemm_rs", "gemm_rs_gfx950.csv")
+_rs_table = None
+own_gemm_calls = 0          # products issued through gemm_rs (tests check that the path ran)
+
+
+def rs_table():
+    """(M, N, K, has_bias) -> (cfg, gm) of the shipped own-GEMM table ({} when off or absent)."""
+    global _rs_table
+    if _rs_table is None:
+        _rs_table = {}
+        path = _os.environ.get("DLTB_OWN_GEMM_TABLE", _RS_FILE)
+        if _os.environ.get("DLTB_OWN_GEMM", "1") == "1" and _os.path.exists(path):
+            with open(path) as f:
+                for r in _csv.DictReader(ln for ln in f if not ln.startswith("#")):
+                    _rs_table[(int(r["m"]), int(r["n"]), int(r["k"]), int(r["bias"]))] = (int(r["cfg"]), int(r["gm"]))
+    return _rs_table
+
+
+def _own_nt(a, b_nk, bias=None):
+    """a [M, K] @ b_nk[N, K]^T (+ bias) through gemm_rs when the table holds the shape, else None."""
+    global own_gemm_calls
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b_nk.dtype == torch.bfloat16 and a.dim() == 2
+            and a.stride(1) == 1 and b_nk.stride(1) == 1 and a.stride(0) % 8 == 0 and b_nk.stride(0) % 8 == 0):
+        return None
+    M, K = a.shape
+    N = b_nk.shape[0]
+    hit = rs_table().get((M, N, K, int(bias is not None)))
+    if hit is None:
+        return None
+    own_gemm_calls += 1
+    return ext().gemm_rs(a, b_nk, None, bias, False, hit[0], hit[1])
+
+
 def _tuned(a, b, bias=None):
     """a @ b (+ bias) through the tuned hipBLASLt table, or None when the problem is not in it."""
     if not (_blt.active() and a.is_cuda):
@@ -370,6 +411,9 @@ def _tuned(a, b, bias=None):
 
 
 def linear_fwd(x2d, w, b=None):
+    y = _own_nt(x2d, w, b)
+    if y is not None:
+        return y
     y = _tuned(x2d, w.t(), b)
     if y is not None:
         return y
@@ -416,6 +460,10 @@ def linear_dgrad_splitk(dy2d, wt):
 
 def linear_dgrad(dy2d, w, wt=None):
     """dX = dY W; with a cached contiguous W^T the product runs as dY (W^T)^T (hipBLASLt NT form)."""
+    if wt is not None:
+        y = _own_nt(dy2d, wt)            # dY (W^T)^T: the cached W^T is the NT operand
+        if y is not None:
+            return y
     rhs = wt.t() if wt is not None else w
     y = _tuned(dy2d, rhs)
     return y if y is not None else torch.mm(dy2d, rhs)
