@@ -70,17 +70,17 @@ DLTB_DEV void adam_elem(float& p, float& m, float& v, float g, const AdamHp& h) 
 // moments as two float4, a 16-bit gradient and the 16-bit parameter copy as one 16-byte access;
 // 4: the 8-byte 16-bit accesses of segments not 8-element aligned).  ITERS vectors per lane, all
 // loads issued before the first update (ITERS * (6 + 1) 16-byte loads in flight per lane at W = 8).
-template <typename G, int W>
+template <typename G, int W, int T = kAdamThreads>
 DLTB_DEV void adamw_block(float* __restrict__ master, float* __restrict__ exp_avg, float* __restrict__ exp_avg_sq,
                           const G* __restrict__ grad, bf16_t* __restrict__ dst, int64_t start, int64_t seg_end,
                           int64_t dst_base, const AdamHp& h) {
-  constexpr int ITERS = kAdamChunk / (kAdamThreads * W);
+  constexpr int ITERS = kAdamChunk / (T * W);
   constexpr int NV = W / 4;
   v4f P[ITERS][NV], M[ITERS][NV], V[ITERS][NV];
   float Gr[ITERS][W];
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
-    const int64_t i = start + ((int64_t)it * kAdamThreads + threadIdx.x) * W;
+    const int64_t i = start + ((int64_t)it * T + threadIdx.x) * W;
     if (i < seg_end) {
 #pragma unroll
       for (int q = 0; q < NV; ++q) {
@@ -94,7 +94,7 @@ DLTB_DEV void adamw_block(float* __restrict__ master, float* __restrict__ exp_av
   }
 #pragma unroll
   for (int it = 0; it < ITERS; ++it) {
-    const int64_t off = ((int64_t)it * kAdamThreads + threadIdx.x) * W;
+    const int64_t off = ((int64_t)it * T + threadIdx.x) * W;
     const int64_t i = start + off;
     if (i >= seg_end) break;
     float p[W], m[W], v[W];
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
     const G* __restrict__ grad, const int* __restrict__ blk_seg, const int64_t* __restrict__ blk_start,
     const int64_t* __restrict__ seg_ostart, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, const float* __restrict__ hp,
-    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int narrow) {
+    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int wide_ab) {
   if (hp) {   // step-dependent hyper-parameters from device memory (HIP-graph replays)
     if (hp[3] != 0.f) return;   // dynamic loss scaling found an inf / nan: the step is skipped
     lr = hp[0];
@@ -148,10 +148,15 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
   const int64_t dst_base = start - s0;
   const AdamHp h{lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, gscale ? *gscale : 1.f};
   // every state element is touched once per step: streamed past the caches (nontemporal loads and
-  // stores).  16-byte accesses need 8-element alignment of the owner offset, the segment length and
-  // the destination (wave-uniform test per block; the layouts align segments to 128 elements)
-  const bool wide = !narrow && ((s0 | seg_len[seg]) & 7) == 0 && (((uintptr_t)dst) & 15) == 0;
+  // stores).  The step's path is W = 4 (every fp32 access one coalesced 16-byte vector per lane, the
+  // 16-bit streams 8 bytes per lane): the W = 8 path (two adjacent float4 per lane, 32-byte lane stride
+  // per instruction) measured 4.22 TB/s against 5.52 for W = 4 on the TinyGPT-A state
+  // (profiles/adamw_r5.txt) and is kept only as the DLTB_ADAM_WIDE=1 A/B.  16-byte accesses need
+  // 8-element alignment of the owner offset, the segment length and the destination.
+  const bool wide = wide_ab && ((s0 | seg_len[seg]) & 7) == 0 && (((uintptr_t)dst) & 15) == 0;
   if (wide) adamw_block<G, 8>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
+  else if (blockDim.x == kAdamThreads / 2)   // A/B (DLTB_ADAM_T128=1): half the lanes, twice the loads in flight each
+    adamw_block<G, 4, kAdamThreads / 2>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
   else adamw_block<G, 4>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
 }
 
@@ -263,15 +268,16 @@ void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* gr
                 float lr, float beta1, float beta2, float eps, float wd, float step_size,
                 float inv_sqrt_bc2, hipStream_t st) {
   if (nblocks <= 0) return;
-  static const int narrow = getenv("DLTB_ADAM_NARROW") ? atoi(getenv("DLTB_ADAM_NARROW")) : 0;   // A/B: 8-byte path
+  static const int wide = getenv("DLTB_ADAM_WIDE") ? atoi(getenv("DLTB_ADAM_WIDE")) : 0;   // A/B: 16-byte path
+  static const int thr = getenv("DLTB_ADAM_T128") && atoi(getenv("DLTB_ADAM_T128")) ? kAdamThreads / 2 : kAdamThreads;
   if (grad_bf16)
-    hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
+    hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(nblocks), dim3(thr), 0, st, master,
                        exp_avg, exp_avg_sq, (const bf16_t*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, narrow);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide);
   else
-    hipLaunchKernelGGL(adamw_kernel<float>, dim3(nblocks), dim3(kAdamThreads), 0, st, master,
+    hipLaunchKernelGGL(adamw_kernel<float>, dim3(nblocks), dim3(thr), 0, st, master,
                        exp_avg, exp_avg_sq, (const float*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, narrow);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide);
 }
 
 int dltb_sumsq_partials() { return kSumsqBlocks; }

@@ -35,6 +35,7 @@ namespace {
 typedef h16_t rs_frag __attribute__((ext_vector_type(8)));    // 8 x bf16: one MFMA A/B fragment
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // 16 bytes in 4 VGPRs
 typedef __attribute__((address_space(3))) u32x4 lds_u4t;
+typedef __attribute__((address_space(3))) f32x4 lds_f4t;
 
 struct RsArgs {
   const bf16_t* a;
@@ -97,6 +98,58 @@ struct RsEpi {
           v[e] = pack_bf2(lo_bf(v[e]) + lo_bf(old[e]), hi_bf(v[e]) + hi_bf(old[e]));
       }
       *reinterpret_cast<u32x4*>(dst) = v;
+    }
+  }
+};
+
+// fp32 variant (the 3-buffer kernels, whose stage buffers hold a [BM][BN + 4] fp32 image): phase 1 stores the
+// raw accumulators (16-byte writes, 8 rows per lane group: conflict-free at the BN + 4 pitch); phase 2 adds the
+// bias and rounds ONCE.  Phase 2 gives every thread 4 columns of a row (16-byte LDS read, 8-byte global store:
+// a wave covers 256 contiguous columns).  When BN / 4 divides 256 a thread keeps the same 4 columns in every
+// row it stores, so its bias is loaded once at kernel start (prefetched: no bias latency in the epilogue).
+template <int BM, int BN>
+struct RsEpiF {
+  static constexpr int P = BN + 4;                 // row pitch (fp32 elements)
+  static constexpr int BYTES = BM * P * 4;
+  static constexpr int CPR = BN / 4;               // 4-column chunks per row
+  static constexpr bool FIXED = 256 % CPR == 0;    // the thread's columns are the same in every row
+  struct Bias {
+    float v[4];
+  };
+  DLTB_DEV static Bias prefetch(const bf16_t* bias, int n0, int tid) {
+    Bias b{{0.f, 0.f, 0.f, 0.f}};
+    if (FIXED && bias) {
+      const uint2 bb = *reinterpret_cast<const uint2*>(bias + n0 + (tid % CPR) * 4);
+      b.v[0] = lo_bf(bb.x); b.v[1] = hi_bf(bb.x); b.v[2] = lo_bf(bb.y); b.v[3] = hi_bf(bb.y);
+    }
+    return b;
+  }
+  DLTB_DEV static void put(uint32_t lds0, int ml, int nl, const float* a) {
+    *(lds_f4t*)(size_t)(lds0 + (ml * P + nl) * 4) = f32x4{a[0], a[1], a[2], a[3]};
+  }
+  DLTB_DEV static void flush(const RsArgs& g, uint32_t lds0, int m0, int n0, int tid, const Bias& pb) {
+    constexpr int CHUNKS = BM * CPR;
+    static_assert(CHUNKS % 256 == 0, "epilogue chunks");
+#pragma unroll 8
+    for (int c = tid; c < CHUNKS; c += 256) {
+      const int row = c / CPR, ch = c - row * CPR;
+      const f32x4 x = *(lds_f4t*)(size_t)(lds0 + (row * P + ch * 4) * 4);
+      float v[4] = {x[0], x[1], x[2], x[3]};
+      if (FIXED) {
+        v[0] += pb.v[0]; v[1] += pb.v[1]; v[2] += pb.v[2]; v[3] += pb.v[3];
+      } else if (g.bias) {
+        const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n0 + ch * 4);
+        v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
+      }
+      bf16_t* dst = g.c + (size_t)(m0 + row) * g.ldc + n0 + ch * 4;
+      if (g.accumulate) {
+        const uint2 old = *reinterpret_cast<const uint2*>(dst);
+        v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+      }
+      uint2 o;
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(dst) = o;
     }
   }
 };
@@ -508,6 +561,204 @@ void launch_rsp(const RsArgs& g, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Fenced schedule (kind 3): the rsp pipeline with the issue order written out and pinned.  In the rsp build
+// hipcc honoured the sched_group_barrier masks only in part -- MFMAs of the second half were pulled into
+// the first half's slots, the fragment reads they need were queued right in front of them
+// (s_waitcnt lgkmcnt(0) before every few MFMAs) and the LDS writes + global loads issued as one cluster.
+// Here every MFMA is followed by its slot of memory instructions, with a full scheduling fence
+// (__builtin_amdgcn_sched_barrier(0)) around each slot, so the program order IS the issue order:
+//   half 0: MFMA q of stage kt (X), then Y-read / LDS-write / global-load share q     (q < NM)
+//   half 1: MFMA q of stage kt (Y), then X-read share q (half 0 of stage kt + 1)
+//   s_waitcnt lgkmcnt(NR) (this segment's LDS writes done, the X reads may stay in flight) + s_barrier
+// LDS operations complete in order, so the waits the compiler places before each MFMA are partial.
+template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
+  using G = RsGeo<BM, BN, WGM, D, M32>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % WGM, wn = wave / WGM;
+
+  const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  int mb, nb;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {
+    const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  } else {
+    mb = idx / tiles_n;
+    nb = idx - mb * tiles_n;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = g.K / G::BK;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * G::BK == g.K && nk % D == 0 && nk >= 2);
+
+  const int prow = tid >> 3, pch = tid & 7;
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.a + (long)m0 * g.lda), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.b + (long)n0 * g.ldb), (short)0, 0x7fffffff, 0x00020000);
+  uint32_t voa[G::NA], vob[G::NB];
+#pragma unroll
+  for (int i = 0; i < G::NA; ++i) voa[i] = (uint32_t)(((32 * i + prow) * g.lda + pch * 8) * 2);
+#pragma unroll
+  for (int i = 0; i < G::NB; ++i) vob[i] = (uint32_t)(((32 * i + prow) * g.ldb + pch * 8) * 2);
+  const uint32_t wlane = rs_off(prow, pch);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  const typename RsEpiF<BM, BN>::Bias pbias = RsEpiF<BM, BN>::prefetch(g.bias, n0, tid);
+
+  constexpr int RL = M32 ? 32 : 16;
+  const int fr = lane & (RL - 1), fq = M32 ? (lane >> 5) : (lane >> 4);
+  const int arow0 = wm * G::WM, brow0 = wn * G::WN;
+  uint32_t foa[G::KS], fob[G::KS];
+#pragma unroll
+  for (int s = 0; s < G::KS; ++s) {
+    foa[s] = rs_off(fr, (M32 ? 2 : 4) * s + fq) + arow0 * 128;
+    fob[s] = rs_off(fr, (M32 ? 2 : 4) * s + fq) + G::A_BYTES + brow0 * 128;
+  }
+
+  using Acc = typename std::conditional<M32, f32x16, f32x4>::type;
+  Acc acc[G::FM][G::FN];
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) acc[i][j] = Acc{};
+
+  constexpr int KH = G::KS / 2;
+  constexpr int FPS = G::FM + G::FN;                    // fragments per k-substep
+  constexpr int NM = KH * G::FM * G::FN, NR = KH * FPS;
+  static_assert(NR <= 15, "lgkmcnt field");
+  struct Frags {
+    rs_frag f[KH][FPS];                                  // a fragments, then b fragments
+  };
+  u32x4 R[D][G::NI];
+
+  // single memory operations, by index (all indices compile-time after unrolling)
+  auto read1 = [&](Frags& F, uint32_t bufbase, int half, int r) {
+    const int s = r / FPS, f = r - s * FPS;
+    const uint32_t off = f < G::FM ? foa[half * KH + s] + G::T * f * 128
+                                   : fob[half * KH + s] + G::T * (f - G::FM) * 128;
+    F.f[s][f] = __builtin_bit_cast(rs_frag, *(lds_u4t*)(size_t)(bufbase + off));
+  };
+  auto write1 = [&](uint32_t bufbase, const u32x4 (&r)[G::NI], int w) {
+    const uint32_t off = w < G::NA ? 4096 * w : G::A_BYTES + 4096 * (w - G::NA);
+    *(lds_u4t*)(size_t)(bufbase + wlane + off) = r[w];
+  };
+  auto load1 = [&](int kt, u32x4 (&r)[G::NI], int l) {
+    const int so = min(kt, nk - 1) * (G::BK * 2);
+    if (l < G::NA) r[l] = __builtin_amdgcn_raw_buffer_load_b128(ra, voa[l], so, 0);
+    else r[l] = __builtin_amdgcn_raw_buffer_load_b128(rb, vob[l - G::NA], so, 0);
+  };
+  auto mma1 = [&](const Frags& F, int q) {
+    const int s = q / (G::FM * G::FN), i = (q / G::FN) % G::FM, j = q % G::FN;
+    if constexpr (M32) acc[i][j] = mfma32(F.f[s][G::FM + j], F.f[s][i], acc[i][j]);
+    else acc[i][j] = mfma16(F.f[s][G::FM + j], F.f[s][i], acc[i][j]);
+  };
+
+  auto keep1 = [&](const Frags& F, int q) {           // ablation: the operands of MFMA q stay live
+    const int s = q / (G::FM * G::FN), i = (q / G::FN) % G::FM, j = q % G::FN;
+    asm volatile("" ::"v"(F.f[s][i]), "v"(F.f[s][G::FM + j]));
+  };
+
+  Frags X, Y;
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int l = 0; l < G::NI; ++l) load1(d, R[d], l);
+#pragma unroll
+  for (int w = 0; w < G::NI; ++w) write1(lds0, R[0], w);
+#pragma unroll
+  for (int l = 0; l < G::NI; ++l) load1(D, R[0], l);
+#pragma unroll
+  for (int w = 0; w < G::NI; ++w) write1(lds0 + G::STAGE, R[1 % D], w);
+#pragma unroll
+  for (int l = 0; l < G::NI; ++l) load1(D + 1, R[1 % D], l);
+  rs_barrier();
+#pragma unroll
+  for (int r = 0; r < NR; ++r) read1(X, lds0, 0, r);
+  uint32_t b_cur = lds0, b_nxt = lds0 + G::STAGE, b_wr = lds0 + 2 * G::STAGE;
+
+  for (int t = 0; t < nk; t += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int kt = t + u;
+      u32x4 (&RR)[G::NI] = R[(u + 2) % D];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        // (DBG & 8 / 16 / 32 / 64: timing-only ablations without fragment reads / loop global loads /
+        // MFMAs / LDS writes)
+        if constexpr ((DBG & 32) == 0) mma1(X, q);
+        else keep1(X, q);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = (NR * q) / NM; r < (NR * (q + 1)) / NM; ++r)
+          if constexpr ((DBG & 8) == 0) read1(Y, b_cur, 1, r);
+#pragma unroll
+        for (int w = (G::NI * q) / NM; w < (G::NI * (q + 1)) / NM; ++w) {
+          if constexpr ((DBG & 64) == 0) write1(b_wr, RR, w);
+          else asm volatile("" ::"v"(RR[w]));
+          if constexpr ((DBG & 16) == 0) load1(kt + 2 + D, RR, w);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        if constexpr ((DBG & 32) == 0) mma1(Y, q);
+        else keep1(Y, q);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = (NR * q) / NM; r < (NR * (q + 1)) / NM; ++r)
+          if constexpr ((DBG & 8) == 0) read1(X, b_nxt, 0, r);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // this segment's LDS writes complete (the NR X reads issued after them may still be in flight:
+      // they read b_nxt, which nobody writes before the NEXT barrier), then the workgroup barrier
+      asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NR) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t b_old = b_cur;
+      b_cur = b_nxt;
+      b_nxt = b_wr;
+      b_wr = b_old;
+    }
+  }
+
+  rs_barrier();                                          // all fragment reads done before the epilogue image
+  using E = RsEpiF<BM, BN>;
+  static_assert(E::BYTES <= 3 * G::STAGE, "epilogue image exceeds the stage buffers");
+#pragma unroll
+  for (int i = 0; i < G::FM; ++i) {
+#pragma unroll
+    for (int j = 0; j < G::FN; ++j) {
+#pragma unroll
+      for (int q = 0; q < G::ACC / 4; ++q) {
+        const float a4[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        E::put(lds0, arow0 + G::T * i + fr, brow0 + G::T * j + (M32 ? 8 * q + 4 * fq : 4 * fq), a4);
+      }
+    }
+  }
+  rs_barrier();
+  E::flush(g, lds0, m0, n0, tid, pbias);
+}
+
+template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
+void launch_rsf(const RsArgs& g, hipStream_t st) {
+  constexpr int smem = 3 * RsGeo<BM, BN, WGM, D, M32>::STAGE;
+  static_assert(smem <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_rsf_kernel<BM, BN, WGM, D, M32, DBG>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_rsf_kernel<BM, BN, WGM, D, M32, DBG>), dim3(tiles), dim3(256), smem, st, g);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Direct-operand variant: the four waves split ONE operand's rows (PA: A / M, else B / N), so each wave's
 // rows of that operand are private -- they are loaded straight into MFMA fragments (16 rows x 64
 // contiguous bytes per load instruction, natural 16x16x32 k order), with no LDS round trip; only the
@@ -693,7 +944,7 @@ struct RsCfg {
   bool m32;
   int dp = 0;        // > 0: direct-operand kernel, DP stages of private fragments (d = shared stages)
   bool pa = false;   // direct kernel: A private (waves split M), else B private (waves split N)
-  int kind = 0;      // 2: software-pipelined kernel (3 LDS buffers)
+  int kind = 0;      // 2: software-pipelined kernel (3 LDS buffers), 3: same with a fenced schedule
 };
 // 0-2: N = 1024 products (16 x 16 tiles of 128 x 64); 3-4 / 6: N = 4096 (128 x 256); 5: N = 3072 (128 x 192);
 // 8-12: direct-operand kernels
@@ -716,7 +967,22 @@ constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {12
                              // 26-31: software-pipelined kernel (gemm_rsp_kernel; kind 2)
                              {128, 64, 2, 2, false, 0, false, 2}, {128, 64, 2, 4, false, 0, false, 2},
                              {128, 64, 2, 4, true, 0, false, 2}, {128, 256, 2, 2, true, 0, false, 2},
-                             {128, 192, 2, 2, false, 0, false, 2}, {128, 128, 2, 2, true, 0, false, 2}};
+                             {128, 192, 2, 2, false, 0, false, 2}, {128, 128, 2, 2, true, 0, false, 2},
+                             // 32-37: fenced schedule (gemm_rsf_kernel; kind 3), the shapes of 26-31
+                             {128, 64, 2, 2, false, 0, false, 3}, {128, 64, 2, 4, false, 0, false, 3},
+                             {128, 64, 2, 4, true, 0, false, 3}, {128, 256, 2, 2, true, 0, false, 3},
+                             {128, 192, 2, 2, false, 0, false, 3}, {128, 128, 2, 2, true, 0, false, 3},
+                             // 38-42: ablations of cfg 35 (no fragment reads / no loop loads / no MFMA /
+                             // no LDS writes / nothing but the barriers) -- timing only; 43: cfg 35 at D 3
+                             {128, 256, 2, 2, true, 0, false, 3}, {128, 256, 2, 2, true, 0, false, 3},
+                             {128, 256, 2, 2, true, 0, false, 3}, {128, 256, 2, 2, true, 0, false, 3},
+                             {128, 256, 2, 2, true, 0, false, 3}, {128, 256, 2, 3, true, 0, false, 3},
+                             // 44-48: ablations of cfg 34 (as 38-42); 49: cfg 34 at D 2; 50: cfg 34 with the
+                             // waves split 4 x 1 (32 x 64 each); 51: D 8
+                             {128, 64, 2, 4, true, 0, false, 3}, {128, 64, 2, 4, true, 0, false, 3},
+                             {128, 64, 2, 4, true, 0, false, 3}, {128, 64, 2, 4, true, 0, false, 3},
+                             {128, 64, 2, 4, true, 0, false, 3}, {128, 64, 2, 2, true, 0, false, 3},
+                             {128, 64, 4, 4, true, 0, false, 3}, {128, 64, 2, 8, true, 0, false, 3}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -752,7 +1018,27 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 28: launch_rsp<128, 64, 2, 4, true>(g, st); break;
     case 29: launch_rsp<128, 256, 2, 2, true>(g, st); break;
     case 30: launch_rsp<128, 192, 2, 2, false>(g, st); break;
-    default: launch_rsp<128, 128, 2, 2, true>(g, st); break;
+    case 31: launch_rsp<128, 128, 2, 2, true>(g, st); break;
+    case 32: launch_rsf<128, 64, 2, 2, false>(g, st); break;
+    case 33: launch_rsf<128, 64, 2, 4, false>(g, st); break;
+    case 34: launch_rsf<128, 64, 2, 4, true>(g, st); break;
+    case 35: launch_rsf<128, 256, 2, 2, true>(g, st); break;
+    case 36: launch_rsf<128, 192, 2, 2, false>(g, st); break;
+    case 37: launch_rsf<128, 128, 2, 2, true>(g, st); break;
+    case 38: launch_rsf<128, 256, 2, 2, true, 8>(g, st); break;
+    case 39: launch_rsf<128, 256, 2, 2, true, 16>(g, st); break;
+    case 40: launch_rsf<128, 256, 2, 2, true, 32>(g, st); break;
+    case 41: launch_rsf<128, 256, 2, 2, true, 64>(g, st); break;
+    case 42: launch_rsf<128, 256, 2, 2, true, 120>(g, st); break;
+    case 43: launch_rsf<128, 256, 2, 3, true>(g, st); break;
+    case 44: launch_rsf<128, 64, 2, 4, true, 8>(g, st); break;
+    case 45: launch_rsf<128, 64, 2, 4, true, 16>(g, st); break;
+    case 46: launch_rsf<128, 64, 2, 4, true, 32>(g, st); break;
+    case 47: launch_rsf<128, 64, 2, 4, true, 64>(g, st); break;
+    case 48: launch_rsf<128, 64, 2, 4, true, 120>(g, st); break;
+    case 49: launch_rsf<128, 64, 2, 2, true>(g, st); break;
+    case 50: launch_rsf<128, 64, 4, 4, true>(g, st); break;
+    default: launch_rsf<128, 64, 2, 8, true>(g, st); break;
   }
 }
 
@@ -762,7 +1048,7 @@ static bool rs_fits(int c, int M, int N, int K) {
   if (c < 0 || c >= kRsNumCfgs) return false;
   const RsCfg t = kRsCfgs[c];
   const int dm = t.dp > t.d ? t.dp : t.d;
-  const int u = t.kind == 2 ? t.d : t.dp > 0 ? (dm < 2 ? 2 : dm) : (t.d % 2 == 0 ? t.d : 2 * t.d);
+  const int u = t.kind >= 2 ? t.d : t.dp > 0 ? (dm < 2 ? 2 : dm) : (t.d % 2 == 0 ? t.d : 2 * t.d);
   return M > 0 && N > 0 && K > 0 && M % t.bm == 0 && N % t.bn == 0 && K % 64 == 0 && (K / 64) % u == 0;
 }
 

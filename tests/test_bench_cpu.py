@@ -89,3 +89,22 @@ def test_bench_prediction_lookup():
     row = bench.predicted_row("zero2-dp8", "bf16", 8)
     assert row is not None and row["ms_per_step"] > 0 and row["table"].startswith("profiles/emulated_scaling")
     assert bench.predicted_row("zero2-dp8", "fp32", 8) is None
+
+
+def test_own_gemm_table_parsing(tmp_path, monkeypatch):
+    """ops/functional.py reads the own-GEMM table (comments skipped) and DLTB_OWN_GEMM=0 turns it off."""
+    import dltb.ops.functional as F
+    t = tmp_path / "t.csv"
+    t.write_text("# note\nm,n,k,bias,cfg,gm\n2048,1024,1024,1,34,1\n2048,1024,4096,0,34,4\n")
+    monkeypatch.setenv("DLTB_OWN_GEMM_TABLE", str(t))
+    F._rs_table = None
+    assert F.rs_table() == {(2048, 1024, 1024, 1): (34, 1), (2048, 1024, 4096, 0): (34, 4)}
+    monkeypatch.setenv("DLTB_OWN_GEMM", "0")
+    F._rs_table = None
+    assert F.rs_table() == {}
+    monkeypatch.delenv("DLTB_OWN_GEMM")
+    monkeypatch.delenv("DLTB_OWN_GEMM_TABLE")
+    F._rs_table = None
+    shipped = F.rs_table()
+    assert shipped and all(v[0] in (34, 49, 50) for v in shipped.values())
+    F._rs_table = None

@@ -1,0 +1,82 @@
+"""Own MFMA GEMM (csrc/gemm_rs.hip) against an fp32 torch product: every row of the shipped own-GEMM
+table (the configs the training step runs), bias / accumulate epilogues, grids with more tiles than CUs
+(co-resident workgroups: the case that exposed the LDS race fixed by rs_barrier), and the model path
+(ops/functional.py dispatch) actually issuing them."""
+import csv
+import os
+
+import pytest
+import torch
+
+import dltb  # noqa: F401
+import dltb.ops.functional as F
+from dltb.ops._ext import ext
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TABLE = os.path.join(ROOT, "configs", "gemm_rs", "gemm_rs_gfx950.csv")
+
+
+def _rows():
+    with open(TABLE) as f:
+        return [{k: int(v) for k, v in r.items()} for r in csv.DictReader(ln for ln in f if not ln.startswith("#"))]
+
+
+def _check(M, N, K, cfg, gm, bias, accumulate=False):
+    torch.manual_seed(M + N + K + cfg)
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    bb = torch.randn(N, device="cuda", dtype=torch.bfloat16) if bias else None
+    c0 = torch.randn(M, N, device="cuda", dtype=torch.bfloat16) if accumulate else None
+    ref = a.float() @ b.float().t()
+    if bias:
+        ref += bb.float()
+    if accumulate:
+        ref += c0.float()
+    out = c0.clone() if accumulate else None
+    y = ext().gemm_rs(a, b, out, bb, accumulate, cfg, gm)
+    torch.cuda.synchronize()
+    err = (y.float() - ref).abs().max().item()
+    # bf16 output: half an ulp of the largest magnitude, plus fp32 accumulation-order noise
+    tol = ref.abs().max().item() * 2 ** -8 + 1e-2
+    assert err <= tol, f"M{M} N{N} K{K} cfg {cfg} gm {gm}: max err {err:.4g} > {tol:.4g}"
+
+
+@pytest.mark.parametrize("row", _rows(), ids=lambda r: f"{r['m']}x{r['n']}x{r['k']}b{r['bias']}c{r['cfg']}")
+def test_shipped_table_rows(row):
+    assert ext().gemm_rs_supported(row["m"], row["n"], row["k"], row["cfg"])
+    _check(row["m"], row["n"], row["k"], row["cfg"], row["gm"], bool(row["bias"]))
+
+
+@pytest.mark.parametrize("cfg", [34, 35, 36, 49, 50])
+def test_fenced_kernels_epilogues(cfg):
+    M, N, K = (2048, 3072, 1024) if cfg == 36 else (2048, 4096 if cfg == 35 else 1024, 1024)
+    _check(M, N, K, cfg, 4, bias=True)
+    _check(M, N, K, cfg, 1, bias=False, accumulate=True)
+
+
+@pytest.mark.parametrize("cfg", [34, 49])
+def test_coresident_workgroups(cfg):
+    # 4096 x 2048 with 128 x 64 tiles = 1024 workgroups (4 per CU over time, 2 resident at once)
+    for _ in range(3):
+        _check(4096, 2048, 1024, cfg, 4, bias=True)
+
+
+def test_model_step_issues_own_gemm():
+    from dltb.models import build_model, get_model_config
+    from dltb.parallel import engine_config, make_engine
+    F._rs_table = None
+    if not F.rs_table():
+        pytest.skip("own-GEMM table off (DLTB_OWN_GEMM=0) or absent")
+    torch.manual_seed(0)
+    cfg = get_model_config("A", 2048)
+    cfg.n_layer = 1
+    eng = make_engine(build_model(cfg), engine_config("zero2", 1, "reference"), "cuda:0")
+    idx = torch.randint(0, cfg.vocab_size, (1, 2048), device="cuda:0")
+    c0 = F.own_gemm_calls
+    loss = eng(idx, idx)[1]
+    eng.backward(loss)
+    torch.cuda.synchronize()
+    assert F.own_gemm_calls - c0 == len(_rows()), "every shipped product should run on the own kernel"
+    assert 5.0 < float(loss.item()) < 15.0
