@@ -447,7 +447,13 @@ class ReplicatedEngine(Engine):
         if self._tail_defer and self._is_boundary:
             self._drain_all()                   # the optimizer reads the window's full sum next (one
             #                                     fold launch; the token rows are applied in it)
-        if self._sparse is not None and not (self._tail_defer and not self._is_boundary and _SPARSE_DEFER):
+        # (DDP pipeline at the optimizer boundary: the token rows' all-gathers were issued by the
+        # embedding backward, i.e. behind every bucket's all-reduce on the comm stream -- waiting for
+        # them here exposed the whole all-reduce tail.  _update applies them right before the tied
+        # table's own AdamW segment, which it runs last.)
+        pipe_rows = self._ddp_pipe and self._is_boundary
+        if self._sparse is not None and not pipe_rows and \
+                not (self._tail_defer and not self._is_boundary and _SPARSE_DEFER):
             b = self._bucket_of[id(self._sparse[0][0])]
             if b in self._rs_inflight:
                 self._drain_bucket(b)          # the token table's chunk, then its sparse rows
@@ -483,12 +489,21 @@ class ReplicatedEngine(Engine):
 
     def _update(self, lr):
         if self._ddp_pipe:
-            # per bucket, in all-reduce issue order: wait for that bucket's sum, then its AdamW rows
+            # per bucket, in all-reduce issue order: wait for that bucket's sum, then its AdamW rows;
+            # the tied token table's bucket goes last: its gathered token rows (issued after every
+            # all-reduce) are scatter-added into it first
             g = self._owner_grad()
             gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)   # (no clip: a fill)
             self.opt.prepare(lr)
-            for b in range(len(self.layout.buckets)):
+            order = list(range(len(self.layout.buckets)))
+            bt = self._bucket_of[id(self._sparse[0][0])] if self._sparse is not None else None
+            if bt is not None:
+                order.remove(bt)
+                order.append(bt)
+            for b in order:
                 self._wait_allreduce(b)
+                if b == bt:
+                    self._apply_sparse()
                 self.opt.launch_segment(b, g, gscale)
             return
         self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
