@@ -54,6 +54,10 @@
 #ifndef DLTB_FWD_KS64
 #define DLTB_FWD_KS64 4
 #endif
+// causal D = 64 caps the splits at 3 (forward) / 2 (dQ) -- A/B build: -D DLTB_CAUSAL_KS_CAP=0
+#ifndef DLTB_CAUSAL_KS_CAP
+#define DLTB_CAUSAL_KS_CAP 1
+#endif
 #ifndef DLTB_DQ_KS64
 #define DLTB_DQ_KS64 3
 #endif
@@ -287,7 +291,7 @@ DLTB_DEV void block_coords(int nqb, int nbh, bool causal, int& qb, int& bh) {
 // instantiations spill at 4 (16 / 28 B of scratch per lane without / with dropout) and run at 3 (151-152
 // VGPRs, no scratch): profiles/attention_d64_resources_r5.txt
 template <int D, bool C = false>
-constexpr int fwd_ks() { return D == 64 ? (C && DLTB_FWD_KS64 > 3 ? 3 : DLTB_FWD_KS64) : 2; }
+constexpr int fwd_ks() { return D == 64 ? (C && DLTB_CAUSAL_KS_CAP && DLTB_FWD_KS64 > 3 ? 3 : DLTB_FWD_KS64) : 2; }
 template <int D, int KS>
 constexpr int fwd_nst() {   // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
   return D == 64 && KS == 2 && DLTB_FWD_PP ? DLTB_FWD_PP_NST : (D == 64 && KS < 4 ? 3 : 2);
@@ -903,7 +907,7 @@ __global__ __launch_bounds__(256) void dkdv_reduce_kernel(const float* __restric
 // Query-major, KS key-splits per workgroup as in the forward; dQ partials merge through LDS.
 // causal D = 64 with dropout spills at 3 (40 B of scratch per lane): 2 splits there (188 VGPRs, no scratch)
 template <int D, bool C = false>
-constexpr int dq_ks() { return D == 64 ? (C && DLTB_DQ_KS64 > 2 ? 2 : DLTB_DQ_KS64) : 2; }
+constexpr int dq_ks() { return D == 64 ? (C && DLTB_CAUSAL_KS_CAP && DLTB_DQ_KS64 > 2 ? 2 : DLTB_DQ_KS64) : 2; }
 template <int D>
 constexpr int dq_nst() { return D == 64 ? 3 : 2; }   // LDS ring depth, as the forward's
 template <int D>
@@ -1134,6 +1138,9 @@ void set_attrs() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, fwd_smem_bytes<D, fwd_ks<D, C>()>());
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR, dq_ks<D, C>()>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, dq_smem_bytes<D, dq_ks<D, C>()>());
+  if constexpr (D == 64 && C && DLTB_CAUSAL_KS_CAP && DLTB_DQ_KS64 > dq_ks<D, C>())
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, C, DR, DLTB_DQ_KS64>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, dq_smem_bytes<D, DLTB_DQ_KS64>());
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<D, C, DR, dkdv_ks<D>()>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, dkdv_smem_bytes<D>());
 }
@@ -1223,12 +1230,22 @@ void launch_dkdv(const AttnArgs& a, hipStream_t st) {
                        a.part, a.gsplit, rows, cols, a.out, a.out_stride, a.out2, a.out2_stride);
   }
 }
-template <int D, bool C, bool DR>
-void launch_dq(const AttnArgs& a, hipStream_t st) {
-  constexpr int KS = dq_ks<D, C>();
+template <int D, bool C, bool DR, int KS>
+void launch_dq_ks(const AttnArgs& a, hipStream_t st) {
   constexpr int smem = dq_smem_bytes<D, KS>();
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hq), dim3(256 * KS),
                      smem, st, a);
+}
+// Causal D = 64 dQ: 2 key splits short, 3 from T = 1024 (A/B, profiles/attention_causal_d64_ks_r5.txt: T 2048
+// 35.4 -> 32.4 us with 3; B4 T512 12.6 with 2 against 13.1)
+constexpr int kDqCausalLongT = 1024;
+template <int D, bool C, bool DR>
+void launch_dq(const AttnArgs& a, hipStream_t st) {
+  constexpr int KS = dq_ks<D, C>();
+  if constexpr (D == 64 && C && DLTB_CAUSAL_KS_CAP && DLTB_DQ_KS64 > KS) {
+    if (a.T >= kDqCausalLongT) return launch_dq_ks<D, C, DR, DLTB_DQ_KS64>(a, st);
+  }
+  launch_dq_ks<D, C, DR, KS>(a, st);
 }
 }  // namespace
 

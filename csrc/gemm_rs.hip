@@ -924,6 +924,218 @@ void launch_rsd(const RsArgs& g, hipStream_t st) {
   hipLaunchKernelGGL((gemm_rsd_kernel<BM, BN, PA, DP, DS>), dim3(tiles), dim3(256), smem, st, g);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Fenced direct-operand kernel (kind 4).  Ablations of the fenced kernel (profiles/gemm_rs_instep_ab_r5.txt) put
+// the LDS at the top of the per-k-step budget: every staged byte crosses the VGPR -> LDS store path (~79 B/clk per
+// CU) once and the fragment reads twice.  Here the four waves split ONE operand's rows (PA: A / the tile's M, else
+// B / N), so each wave's rows of that operand are private to it and go global -> VGPR straight in MFMA fragment
+// order, never touching the LDS; only the other ("shared") operand is staged through the three LDS buffers.  At
+// 128 x 64 with A private the LDS carries 8 KB of stores and 32 KB of fragment reads per 64-deep k-step instead of
+// 24 + 48 KB.
+// k order: a 32x32x16 fragment holds, in lane l, 8 consecutive k of row (l & 31) from k-half h = l >> 5.  The
+// k-chunk (8 elements) that MFMA substep s takes from half h is chunk 4 h + s of the 64-deep stage -- a
+// permutation of the stage's k applied to BOTH operands alike (the product is unchanged), chosen so that a lane's
+// four private fragments of a stage are 64 contiguous bytes of its row: 4 buffer loads at offsets 0/16/32/48.
+// Private stages: D register sets; stage kt + D's substeps 0-1 are loaded in segment kt's second half (after the
+// MFMAs that last read that set's substeps 0-1), substeps 2-3 in segment kt + 1's first half.
+template <int BM, int BN, bool PA, int D>
+struct RsgGeo {
+  static constexpr int P_ROWS = PA ? BM : BN, S_ROWS = PA ? BN : BM;
+  static constexpr int PW = P_ROWS / 4;              // private rows per wave
+  static constexpr int FP = PW / 32, FS = S_ROWS / 32;
+  static constexpr int NS = S_ROWS / 32;             // shared 16-byte pieces per thread per stage
+  static constexpr int STAGE = S_ROWS * 128;
+  static_assert(PW % 32 == 0 && S_ROWS % 32 == 0, "tile shape");
+};
+
+template <int BM, int BN, bool PA, int D>
+__global__ __launch_bounds__(256, 1) void gemm_rsg_kernel(RsArgs g) {
+  using G = RsgGeo<BM, BN, PA, D>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  int mb, nb;
+  if (g.gm > 1 && tiles_m % g.gm == 0) {
+    const int span = g.gm * tiles_n, grp = idx / span, in = idx - grp * span;
+    mb = grp * g.gm + in % g.gm;
+    nb = in / g.gm;
+  } else {
+    mb = idx / tiles_n;
+    nb = idx - mb * tiles_n;
+  }
+  const int m0 = mb * BM, n0 = nb * BN;
+  const int nk = g.K / 64;
+  DLTB_DCHECK(m0 + BM <= g.M && n0 + BN <= g.N && nk * 64 == g.K && nk % D == 0 && nk >= 2);
+
+  const bf16_t* pbase = PA ? g.a + (long)m0 * g.lda : g.b + (long)n0 * g.ldb;
+  const bf16_t* sbase = PA ? g.b + (long)n0 * g.ldb : g.a + (long)m0 * g.lda;
+  const long pld = PA ? g.lda : g.ldb, sld = PA ? g.ldb : g.lda;
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc((void*)pbase, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsh = __builtin_amdgcn_make_buffer_rsrc((void*)sbase, (short)0, 0x7fffffff, 0x00020000);
+  const int fr = lane & 31, fh = lane >> 5;
+  uint32_t vop[G::FP];                                  // private: row (wave rows + 32 i + fr), k-half fh
+#pragma unroll
+  for (int i = 0; i < G::FP; ++i) vop[i] = (uint32_t)(((wave * G::PW + 32 * i + fr) * pld) * 2 + fh * 64);
+  const int prow = tid >> 3, pch = tid & 7;
+  uint32_t vos[G::NS];                                  // shared staging: row 32 i + tid / 8, chunk tid % 8
+#pragma unroll
+  for (int i = 0; i < G::NS; ++i) vos[i] = (uint32_t)(((32 * i + prow) * sld + pch * 8) * 2);
+  const uint32_t wlane = rs_off(prow, pch);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  const typename RsEpiF<BM, BN>::Bias pbias = RsEpiF<BM, BN>::prefetch(g.bias, n0, tid);
+  uint32_t fos[4];                                      // shared fragment: row fr, chunk 4 fh + s
+#pragma unroll
+  for (int s = 0; s < 4; ++s) fos[s] = rs_off(fr, 4 * fh + s);
+
+  f32x16 acc[G::FP][G::FS];
+#pragma unroll
+  for (int i = 0; i < G::FP; ++i)
+#pragma unroll
+    for (int j = 0; j < G::FS; ++j) acc[i][j] = f32x16{};
+
+  rs_frag P[D][4][G::FP];                               // private fragments: stage set, substep, row block
+  u32x4 R[D][G::NS];                                    // shared staging registers
+  struct Half {
+    rs_frag f[2][G::FS];                                // shared fragments of two substeps
+  };
+  constexpr int NR = 2 * G::FS;                         // shared fragment reads per half
+  static_assert(NR <= 15, "lgkmcnt field");
+
+  auto pload1 = [&](int kt, rs_frag (&p)[4][G::FP], int s, int i) {
+    const int so = min(kt, nk - 1) * 128 + 16 * s;
+    p[s][i] = __builtin_bit_cast(rs_frag, __builtin_amdgcn_raw_buffer_load_b128(rp, vop[i], so, 0));
+  };
+  auto sload1 = [&](int kt, u32x4 (&r)[G::NS], int l) {
+    r[l] = __builtin_amdgcn_raw_buffer_load_b128(rsh, vos[l], min(kt, nk - 1) * 128, 0);
+  };
+  auto swrite1 = [&](uint32_t bufbase, const u32x4 (&r)[G::NS], int w) {
+    *(lds_u4t*)(size_t)(bufbase + wlane + 4096 * w) = r[w];
+  };
+  auto sread1 = [&](Half& H, uint32_t bufbase, int half, int r) {
+    const int s = r / G::FS, j = r - s * G::FS;
+    H.f[s][j] = __builtin_bit_cast(rs_frag, *(lds_u4t*)(size_t)(bufbase + fos[2 * half + s] + 32 * j * 128));
+  };
+  auto mma1 = [&](const Half& H, const rs_frag (&p)[4][G::FP], int half, int q) {
+    const int s = q / (G::FP * G::FS), i = (q / G::FS) % G::FP, j = q % G::FS;
+    // D[n][m]: the MFMA's A operand is the B-matrix fragment (lane = n), its B operand the A-matrix one
+    if constexpr (PA) acc[i][j] = mfma32(H.f[s][j], p[2 * half + s][i], acc[i][j]);
+    else acc[i][j] = mfma32(p[2 * half + s][i], H.f[s][j], acc[i][j]);
+  };
+  constexpr int NM = 2 * G::FP * G::FS;                 // MFMAs per half
+  constexpr int NPL = 2 * G::FP;                        // private loads per half (two substeps)
+
+  // prologue: private stages 0 .. D-1 and shared stages 0 .. D-1 in flight, shared stages 0 / 1 in buffers 0 / 1
+  Half X, Y;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < G::FP; ++i) pload1(d, P[d], s, i);
+#pragma unroll
+    for (int l = 0; l < G::NS; ++l) sload1(d, R[d], l);
+  }
+#pragma unroll
+  for (int w = 0; w < G::NS; ++w) swrite1(lds0, R[0], w);
+#pragma unroll
+  for (int l = 0; l < G::NS; ++l) sload1(D, R[0], l);
+#pragma unroll
+  for (int w = 0; w < G::NS; ++w) swrite1(lds0 + G::STAGE, R[1 % D], w);
+#pragma unroll
+  for (int l = 0; l < G::NS; ++l) sload1(D + 1, R[1 % D], l);
+  rs_barrier();
+#pragma unroll
+  for (int r = 0; r < NR; ++r) sread1(X, lds0, 0, r);
+  uint32_t b_cur = lds0, b_nxt = lds0 + G::STAGE, b_wr = lds0 + 2 * G::STAGE;
+
+  for (int t = 0; t < nk; t += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int kt = t + u;
+      rs_frag (&PC)[4][G::FP] = P[u];                   // this stage's private fragments
+      rs_frag (&PPrev)[4][G::FP] = P[(u + D - 1) % D];  // stage kt - 1's set: its substeps 2-3 reload now
+      u32x4 (&RR)[G::NS] = R[(u + 2) % D];
+      __builtin_amdgcn_sched_barrier(0);
+      // half 0: MFMAs of substeps 0-1 || shared reads of substeps 2-3, shared write / load, private loads
+      // of stage kt - 1 + D substeps 2-3 (their set was last read by segment kt - 1's second half)
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        mma1(X, PC, 0, q);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = (NR * q) / NM; r < (NR * (q + 1)) / NM; ++r) sread1(Y, b_cur, 1, r);
+#pragma unroll
+        for (int w = (G::NS * q) / NM; w < (G::NS * (q + 1)) / NM; ++w) {
+          swrite1(b_wr, RR, w);
+          sload1(kt + 2 + D, RR, w);
+        }
+#pragma unroll
+        for (int l = (NPL * q) / NM; l < (NPL * (q + 1)) / NM; ++l)   // (kt = 0: stage D - 1 again, same data)
+          pload1(kt - 1 + D, PPrev, 2 + l / G::FP, l % G::FP);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // half 1: MFMAs of substeps 2-3 || shared reads of the next stage's substeps 0-1, private loads of
+      // stage kt + D substeps 0-1 into this stage's set
+#pragma unroll
+      for (int q = 0; q < NM; ++q) {
+        mma1(Y, PC, 1, q);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int r = (NR * q) / NM; r < (NR * (q + 1)) / NM; ++r) sread1(X, b_nxt, 0, r);
+#pragma unroll
+        for (int l = (NPL * q) / NM; l < (NPL * (q + 1)) / NM; ++l) pload1(kt + D, PC, l / G::FP, l % G::FP);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NR) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t b_old = b_cur;
+      b_cur = b_nxt;
+      b_nxt = b_wr;
+      b_wr = b_old;
+    }
+  }
+
+  rs_barrier();
+  using E = RsEpiF<BM, BN>;
+  static_assert(E::BYTES <= 163840, "epilogue image exceeds the LDS");
+#pragma unroll
+  for (int i = 0; i < G::FP; ++i) {
+#pragma unroll
+    for (int j = 0; j < G::FS; ++j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float a4[4] = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        // lane: column m = fr of its MFMA tile, rows n = 8 q + 4 fh .. + 3
+        const int pr = wave * G::PW + 32 * i, sr = 32 * j;
+        if constexpr (PA) E::put(lds0, pr + fr, sr + 8 * q + 4 * fh, a4);
+        else E::put(lds0, sr + fr, pr + 8 * q + 4 * fh, a4);
+      }
+    }
+  }
+  rs_barrier();
+  E::flush(g, lds0, m0, n0, tid, pbias);
+}
+
+template <int BM, int BN, bool PA, int D>
+void launch_rsg(const RsArgs& g, hipStream_t st) {
+  constexpr int st3 = 3 * RsgGeo<BM, BN, PA, D>::STAGE, epi = RsEpiF<BM, BN>::BYTES;
+  constexpr int smem = st3 > epi ? st3 : epi;
+  static_assert(smem <= 163840, "LDS budget");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_rsg_kernel<BM, BN, PA, D>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  const int tiles = (g.M / BM) * (g.N / BN);
+  hipLaunchKernelGGL((gemm_rsg_kernel<BM, BN, PA, D>), dim3(tiles), dim3(256), smem, st, g);
+}
+
 template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
 void launch_rs(const RsArgs& g, hipStream_t st) {
   // (DBG & 2: debug builds pad the LDS to 100 KB: one workgroup per CU)
@@ -982,7 +1194,13 @@ constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {12
                              {128, 64, 2, 4, true, 0, false, 3}, {128, 64, 2, 4, true, 0, false, 3},
                              {128, 64, 2, 4, true, 0, false, 3}, {128, 64, 2, 4, true, 0, false, 3},
                              {128, 64, 2, 4, true, 0, false, 3}, {128, 64, 2, 2, true, 0, false, 3},
-                             {128, 64, 4, 4, true, 0, false, 3}, {128, 64, 2, 8, true, 0, false, 3}};
+                             {128, 64, 4, 4, true, 0, false, 3}, {128, 64, 2, 8, true, 0, false, 3},
+                             // 52-58: fenced direct-operand kernel (gemm_rsg_kernel; kind 4): 128 x 64 A private
+                             // at D 4 / 2 / 8, 128 x 256 B private at D 2 / 4, 128 x 192 A private at D 2 / 4
+                             {128, 64, 0, 4, true, 4, true, 4}, {128, 64, 0, 2, true, 2, true, 4},
+                             {128, 64, 0, 8, true, 8, true, 4}, {128, 256, 0, 2, true, 2, false, 4},
+                             {128, 256, 0, 4, true, 4, false, 4}, {128, 192, 0, 2, true, 2, true, 4},
+                             {128, 192, 0, 4, true, 4, true, 4}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -1038,7 +1256,14 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 48: launch_rsf<128, 64, 2, 4, true, 120>(g, st); break;
     case 49: launch_rsf<128, 64, 2, 2, true>(g, st); break;
     case 50: launch_rsf<128, 64, 4, 4, true>(g, st); break;
-    default: launch_rsf<128, 64, 2, 8, true>(g, st); break;
+    case 51: launch_rsf<128, 64, 2, 8, true>(g, st); break;
+    case 52: launch_rsg<128, 64, true, 4>(g, st); break;
+    case 53: launch_rsg<128, 64, true, 2>(g, st); break;
+    case 54: launch_rsg<128, 64, true, 8>(g, st); break;
+    case 55: launch_rsg<128, 256, false, 2>(g, st); break;
+    case 56: launch_rsg<128, 256, false, 4>(g, st); break;
+    case 57: launch_rsg<128, 192, true, 2>(g, st); break;
+    default: launch_rsg<128, 192, true, 4>(g, st); break;
   }
 }
 

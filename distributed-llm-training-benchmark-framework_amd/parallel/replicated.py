@@ -83,6 +83,12 @@ class ReplicatedEngine(Engine):
             # shares the first bucket with two blocks and the blocks' dW batches come out 2/4/4/4/2
             # (a 2-block batch costs 75 us per block against 58 for 4, profiles/wgrad_batch_size_r2.txt)
             solo_head = int(cfg.extra.get("solo_head_units", os.environ.get("DLTB_SOLO_HEAD", 1)))
+            if self._ddp_pipe_wanted():
+                # DDP with the optimizer pipelined per bucket: the last bucket's all-reduce is the exposed
+                # tail, so blocks 0 and 1 get buckets of their own (1-block dW batches, +~0.1 ms) and the
+                # tail shrinks from a 4-block bucket to one block: emulated ddp_bf16 N = 8 10.09 -> 9.97 ms
+                # (profiles/emulated_ddp_pipeline_r5.txt)
+                solo_tail = 3
         # the first bucket(s) after the head: twice the size (fewer collectives early in the backward,
         # while compute hides them; the buckets at its end -- the first parameter all-gathers of the
         # next forward -- keep the usual size): emulated ZeRO-2 N = 8 -0.7 %, N = 2 -0.5 %
@@ -148,9 +154,7 @@ class ReplicatedEngine(Engine):
         # wire and only the last bucket's rows stay exposed behind the comm tail.  (fp16 with dynamic
         # loss scaling needs the global inf check over every bucket first, and clipping the global
         # norm: both keep the whole-model update after the last wait.)
-        self._ddp_pipe = (self.stage == 0 and self.world > 1 and self._overlap and self.scaler is None
-                          and not cfg.grad_clip > 0 and not cfg.extra.get("track_grad_norm", False)
-                          and os.environ.get("DLTB_DDP_OPT_PIPELINE", "1") == "1")
+        self._ddp_pipe = self._ddp_pipe_wanted()
         self._ar_works = {}      # bucket -> its all-reduce (untracked) while the pipeline is on
         if self._ddp_pipe:
             g_full = self.comm_f32 if self.comm_f32 is not None else self.flat_grad
@@ -481,6 +485,12 @@ class ReplicatedEngine(Engine):
         if self.acc is not None and self.stage == 2:
             return self.acc
         return self.rs_out if self.world > 1 else self.flat_grad
+
+    def _ddp_pipe_wanted(self):
+        cfg = self.cfg
+        return (int(cfg.zero_stage) == 0 and self.world > 1 and bool(cfg.extra.get("overlap_comm", True))
+                and self.scaler is None and not cfg.grad_clip > 0 and not cfg.extra.get("track_grad_norm", False)
+                and os.environ.get("DLTB_DDP_OPT_PIPELINE", "1") == "1")
 
     def _wait_allreduce(self, b):
         w = self._ar_works.pop(b, None)

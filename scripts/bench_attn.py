@@ -22,7 +22,10 @@ SHAPES = {"tinygpt_a": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.
           "tinygpt_a_p0": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.0),
           "m7b": dict(B=1, T=4096, Hq=32, Hkv=8, D=128, causal=True, p=0.0),
           # three TinyGPT-A micro-batches: 768 query blocks, so several workgroups share a CU
-          "tinygpt_a_b3": dict(B=3, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.1)}
+          "tinygpt_a_b3": dict(B=3, T=2048, Hq=16, Hkv=16, D=64, causal=False, p=0.1),
+          # causal D = 64 (mtiny-like): the shapes the causal split caps of csrc/attention.hip act on
+          "causal_d64": dict(B=1, T=2048, Hq=16, Hkv=16, D=64, causal=True, p=0.0),
+          "causal_d64_short": dict(B=4, T=512, Hq=8, Hkv=8, D=64, causal=True, p=0.0)}
 
 
 def timeit(fn, iters):

@@ -474,6 +474,7 @@ def test_attention(B, T, Hq, Hkv, D, causal, p):
 @pytest.mark.parametrize("B,T,Hq,Hkv,D,causal,p", [
     (1, 2048, 16, 16, 64, False, 0.1),     # TinyGPT-A bench shape (non-causal, dropout 0.1)
     (1, 4096, 32, 8, 128, True, 0.0),      # Mistral-7B shape: causal GQA 32/8, D=128, gsplit dK/dV
+    (1, 1024, 4, 4, 64, True, 0.1),        # causal D=64 from T=1024: the dQ pass at 3 key splits
 ])
 def test_attention_full_shape_fwd_bwd(B, T, Hq, Hkv, D, causal, p):
     """The shapes the benchmarks run, forward AND backward, against the fp32 reference."""
