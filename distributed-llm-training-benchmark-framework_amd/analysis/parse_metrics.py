@@ -10,7 +10,10 @@ Output contract:
 * ``scaling_efficiency_pct`` uses the reference formula per (strategy, seq_len) group with more than
   one row: ``tps / (tps_of_first_row_at_min_ws * ws) * 100`` (single-row groups keep 100.0).  When
   the smallest world size in a group is 2 this reads 50 % for the 2-GPU row — reproduced verbatim
-  for CSV compatibility.
+  for CSV compatibility.  One deliberate deviation: the group key also holds the tier when a result
+  set mixes tiers at one (strategy, seq_len) -- the reference's long-sequence Tier B rows
+  (run_all_benchmarks.sh:49-51) would otherwise be the 1-GPU base of the Tier A rows (a 1-GPU Tier A
+  row read 487 % against the Tier B row of the same strategy and sequence length).
 
 The corrected numbers go to ``metrics_extended.csv``: efficiency normalised to the group's WS=1 row
 (true weak-scaling efficiency), efficiency normalised to the smallest world size
@@ -43,7 +46,8 @@ def load_records(results_dir):
 
 def reference_efficiency(df: pd.DataFrame) -> pd.Series:
     eff = pd.Series(100.0, index=df.index)
-    for (_, _), grp in df.groupby(["strategy", "seq_len"], sort=False):
+    keys = ["strategy", "seq_len"] + (["tier"] if "tier" in df.columns else [])
+    for _, grp in df.groupby(keys, sort=False):
         if len(grp) < 2:
             continue
         base = grp[grp["world_size"] == grp["world_size"].min()].iloc[0]["tokens_per_sec"]

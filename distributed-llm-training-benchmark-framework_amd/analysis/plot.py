@@ -3,7 +3,10 @@
 Same five files, titles and axes as the reference (matplotlib Agg, 10x6 in, 150 dpi):
 ``tokens_per_sec_vs_gpu.png``, ``step_time_vs_gpu.png``, ``vram_vs_seqlen.png`` (only when more
 than one sequence length is present), ``scaling_efficiency.png`` (0-110 %, dashed ideal line) and
-``gbps_vs_gpu.png``; one line per strategy, labelled in upper case.
+``gbps_vs_gpu.png``; one line per strategy, labelled in upper case.  A result set that mixes sequence
+lengths, tiers or world sizes (e.g. the 1-GPU multi-sequence suite, configs/suite/multiseq_1gpu.txt) gets one
+line per strategy AND per value of the columns that vary and are not the plot's x axis (``ZERO3 seq4096``,
+``ZERO3 tier B``): the reference's per-strategy lines would join points of different shapes.
 """
 import argparse
 from pathlib import Path
@@ -29,11 +32,23 @@ PLOTS = [
 ]
 
 
+def _series(df, xcol):
+    """(label, rows) per line: strategy, plus every shape column that varies and is not the x axis."""
+    extra = [c for c in ("seq_len", "tier", "world_size") if c != xcol and c in df.columns and df[c].nunique() > 1]
+    tag = {"seq_len": "seq{}", "tier": "tier {}", "world_size": "ws{}"}
+    out = []
+    for key, sub in df.groupby(["strategy"] + extra, sort=False):
+        key = key if isinstance(key, tuple) else (key,)
+        label = " ".join([str(key[0]).upper()] + [tag[c].format(v) for c, v in zip(extra, key[1:])])
+        out.append((label, sub))
+    return out
+
+
 def _one(df, out, fname, xcol, ycol, xlabel, ylabel, title):
     fig, ax = plt.subplots(figsize=(10, 6))
-    for strategy in df["strategy"].unique():
-        sub = df[df["strategy"] == strategy].sort_values(xcol)
-        ax.plot(sub[xcol], sub[ycol], marker="o", linewidth=2, label=str(strategy).upper())
+    for label, sub in _series(df, xcol):
+        sub = sub.sort_values(xcol)
+        ax.plot(sub[xcol], sub[ycol], marker="o", linewidth=2, label=label)
     if ycol == "scaling_efficiency_pct":
         ax.axhline(y=100, color="gray", linestyle="--", alpha=0.5, label="Ideal (100%)")
         ax.set_ylim(0, 110)
