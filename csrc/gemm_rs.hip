@@ -658,6 +658,12 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
     else acc[i][j] = mfma16(F.f[s][G::FM + j], F.f[s][i], acc[i][j]);
   };
 
+  auto keepall = [&](const Frags& F) {
+#pragma unroll
+    for (int s = 0; s < KH; ++s)
+#pragma unroll
+      for (int f = 0; f < FPS; ++f) asm volatile("" ::"v"(F.f[s][f]));
+  };
   auto keep1 = [&](const Frags& F, int q) {           // ablation: the operands of MFMA q stay live
     const int s = q / (G::FM * G::FN), i = (q / G::FN) % G::FM, j = q % G::FN;
     asm volatile("" ::"v"(F.f[s][i]), "v"(F.f[s][G::FM + j]));
@@ -705,6 +711,10 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      // DBG & 128: every X fragment stays live to the end of its half, so the Y reads issued between the X
+      // MFMAs cannot be given the registers of a fragment an MFMA in flight is still reading (the register
+      // allocator otherwise reuses each fragment's registers right after its last MFMA)
+      if constexpr ((DBG & 128) != 0) keepall(X);
 #pragma unroll
       for (int q = 0; q < NM; ++q) {
         if constexpr ((DBG & 32) == 0) mma1(Y, q);
@@ -715,6 +725,7 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
           if constexpr ((DBG & 8) == 0) read1(X, b_nxt, 0, r);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr ((DBG & 128) != 0) keepall(Y);          // (see the X half)
       // this segment's LDS writes complete (the NR X reads issued after them may still be in flight:
       // they read b_nxt, which nobody writes before the NEXT barrier), then the workgroup barrier
       asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NR) : "memory");
@@ -1200,7 +1211,10 @@ constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {12
                              {128, 64, 0, 4, true, 4, true, 4}, {128, 64, 0, 2, true, 2, true, 4},
                              {128, 64, 0, 8, true, 8, true, 4}, {128, 256, 0, 2, true, 2, false, 4},
                              {128, 256, 0, 4, true, 4, false, 4}, {128, 192, 0, 2, true, 2, true, 4},
-                             {128, 192, 0, 4, true, 4, true, 4}};
+                             {128, 192, 0, 4, true, 4, true, 4},
+                             // 59-61: cfgs 35 / 34 / 36 with the fragment sets kept apart (DBG 128)
+                             {128, 256, 2, 2, true, 0, false, 3}, {128, 64, 2, 4, true, 0, false, 3},
+                             {128, 192, 2, 2, false, 0, false, 3}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -1263,7 +1277,10 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 55: launch_rsg<128, 256, false, 2>(g, st); break;
     case 56: launch_rsg<128, 256, false, 4>(g, st); break;
     case 57: launch_rsg<128, 192, true, 2>(g, st); break;
-    default: launch_rsg<128, 192, true, 4>(g, st); break;
+    case 58: launch_rsg<128, 192, true, 4>(g, st); break;
+    case 59: launch_rsf<128, 256, 2, 2, true, 128>(g, st); break;
+    case 60: launch_rsf<128, 64, 2, 4, true, 128>(g, st); break;
+    default: launch_rsf<128, 192, 2, 2, false, 128>(g, st); break;
   }
 }
 

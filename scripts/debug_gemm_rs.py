@@ -15,7 +15,8 @@ TILE = {0: (128, 64), 1: (128, 64), 2: (128, 64), 3: (128, 256), 4: (128, 256), 
         13: (128, 64), 14: (128, 64), 15: (128, 64), 26: (128, 64), 27: (128, 64), 28: (128, 64),
         29: (128, 256), 30: (128, 192), 31: (128, 128), 32: (128, 64), 33: (128, 64), 34: (128, 64),
         35: (128, 256), 36: (128, 192), 37: (128, 128), 43: (128, 256), 49: (128, 64), 50: (128, 64), 51: (128, 64),
-        52: (128, 64), 53: (128, 64), 54: (128, 64), 55: (128, 256), 56: (128, 256), 57: (128, 192), 58: (128, 192)}
+        52: (128, 64), 53: (128, 64), 54: (128, 64), 55: (128, 256), 56: (128, 256), 57: (128, 192), 58: (128, 192),
+        59: (128, 256), 60: (128, 64), 61: (128, 192)}
 C = ext()
 REPS = int(os.environ.get("REPS", "10"))
 torch.manual_seed(0)
