@@ -107,12 +107,12 @@ struct RsEpi {
 // bias and rounds ONCE.  Phase 2 gives every thread 4 columns of a row (16-byte LDS read, 8-byte global store:
 // a wave covers 256 contiguous columns).  When BN / 4 divides 256 a thread keeps the same 4 columns in every
 // row it stores, so its bias is loaded once at kernel start (prefetched: no bias latency in the epilogue).
-template <int BM, int BN>
+template <int BM, int BN, int NT = 256>
 struct RsEpiF {
   static constexpr int P = BN + 4;                 // row pitch (fp32 elements)
   static constexpr int BYTES = BM * P * 4;
   static constexpr int CPR = BN / 4;               // 4-column chunks per row
-  static constexpr bool FIXED = 256 % CPR == 0;    // the thread's columns are the same in every row
+  static constexpr bool FIXED = NT % CPR == 0;     // the thread's columns are the same in every row
   struct Bias {
     float v[4];
   };
@@ -129,9 +129,9 @@ struct RsEpiF {
   }
   DLTB_DEV static void flush(const RsArgs& g, uint32_t lds0, int m0, int n0, int tid, const Bias& pb) {
     constexpr int CHUNKS = BM * CPR;
-    static_assert(CHUNKS % 256 == 0, "epilogue chunks");
+    static_assert(CHUNKS % NT == 0, "epilogue chunks");
 #pragma unroll 8
-    for (int c = tid; c < CHUNKS; c += 256) {
+    for (int c = tid; c < CHUNKS; c += NT) {
       const int row = c / CPR, ch = c - row * CPR;
       const f32x4 x = *(lds_f4t*)(size_t)(lds0 + (row * P + ch * 4) * 4);
       float v[4] = {x[0], x[1], x[2], x[3]};
@@ -154,21 +154,23 @@ struct RsEpiF {
   }
 };
 
-template <int BM, int BN, int WGM, int D, bool M32>
+template <int BM, int BN, int WGM, int D, bool M32, int NW = 4>
 struct RsGeo {
-  static_assert(4 % WGM == 0, "4 waves");
-  static constexpr int WGN = 4 / WGM;
+  static_assert(NW % WGM == 0, "wave grid");
+  static constexpr int WGN = NW / WGM;
+  static constexpr int PR = 8 * NW;                       // rows per staging pass (8 lanes per 128-byte row)
+  static constexpr int PSTRIDE = PR * 128;                // LDS bytes per staging pass
   static constexpr int BK = 64;
   static constexpr int WM = BM / WGM, WN = BN / WGN;     // wave tile
   static constexpr int T = M32 ? 32 : 16;                 // MFMA output edge
   static constexpr int FM = WM / T, FN = WN / T;          // MFMA tiles per wave
   static constexpr int KS = M32 ? 4 : 2;                  // MFMA k-steps per 64-deep stage
-  static constexpr int NA = BM / 32, NB = BN / 32;        // 16-byte pieces per thread per stage
+  static constexpr int NA = BM / PR, NB = BN / PR;        // 16-byte pieces per thread per stage
   static constexpr int NI = NA + NB;
   static constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   static constexpr int U = D % 2 == 0 ? D : 2 * D;        // k-loop unroll: register set and LDS buffer both static
   static constexpr int ACC = M32 ? 16 : 4;
-  static_assert(WM % T == 0 && WN % T == 0 && BM % 32 == 0 && BN % 32 == 0, "tile shape");
+  static_assert(WM % T == 0 && WN % T == 0 && BM % PR == 0 && BN % PR == 0, "tile shape");
 };
 
 // Workgroup barrier that no LDS access can cross in either direction.  __syncthreads() alone is not a
@@ -571,9 +573,9 @@ void launch_rsp(const RsArgs& g, hipStream_t st) {
 //   half 1: MFMA q of stage kt (Y), then X-read share q (half 0 of stage kt + 1)
 //   s_waitcnt lgkmcnt(NR) (this segment's LDS writes done, the X reads may stay in flight) + s_barrier
 // LDS operations complete in order, so the waits the compiler places before each MFMA are partial.
-template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
-__global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
-  using G = RsGeo<BM, BN, WGM, D, M32>;
+template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 1) void gemm_rsf_kernel(RsArgs g) {
+  using G = RsGeo<BM, BN, WGM, D, M32, NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -603,12 +605,13 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.b + (long)n0 * g.ldb), (short)0, 0x7fffffff, 0x00020000);
   uint32_t voa[G::NA], vob[G::NB];
 #pragma unroll
-  for (int i = 0; i < G::NA; ++i) voa[i] = (uint32_t)(((32 * i + prow) * g.lda + pch * 8) * 2);
+  for (int i = 0; i < G::NA; ++i) voa[i] = (uint32_t)(((G::PR * i + prow) * g.lda + pch * 8) * 2);
 #pragma unroll
-  for (int i = 0; i < G::NB; ++i) vob[i] = (uint32_t)(((32 * i + prow) * g.ldb + pch * 8) * 2);
+  for (int i = 0; i < G::NB; ++i) vob[i] = (uint32_t)(((G::PR * i + prow) * g.ldb + pch * 8) * 2);
   const uint32_t wlane = rs_off(prow, pch);
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
-  const typename RsEpiF<BM, BN>::Bias pbias = RsEpiF<BM, BN>::prefetch(g.bias, n0, tid);
+  using E = RsEpiF<BM, BN, 64 * NW>;
+  const typename E::Bias pbias = E::prefetch(g.bias, n0, tid);
 
   constexpr int RL = M32 ? 32 : 16;
   const int fr = lane & (RL - 1), fq = M32 ? (lane >> 5) : (lane >> 4);
@@ -644,7 +647,7 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
     F.f[s][f] = __builtin_bit_cast(rs_frag, *(lds_u4t*)(size_t)(bufbase + off));
   };
   auto write1 = [&](uint32_t bufbase, const u32x4 (&r)[G::NI], int w) {
-    const uint32_t off = w < G::NA ? 4096 * w : G::A_BYTES + 4096 * (w - G::NA);
+    const uint32_t off = w < G::NA ? G::PSTRIDE * w : G::A_BYTES + G::PSTRIDE * (w - G::NA);
     *(lds_u4t*)(size_t)(bufbase + wlane + off) = r[w];
   };
   auto load1 = [&](int kt, u32x4 (&r)[G::NI], int l) {
@@ -738,7 +741,6 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
   }
 
   rs_barrier();                                          // all fragment reads done before the epilogue image
-  using E = RsEpiF<BM, BN>;
   static_assert(E::BYTES <= 3 * G::STAGE, "epilogue image exceeds the stage buffers");
 #pragma unroll
   for (int i = 0; i < G::FM; ++i) {
@@ -755,18 +757,18 @@ __global__ __launch_bounds__(256, 1) void gemm_rsf_kernel(RsArgs g) {
   E::flush(g, lds0, m0, n0, tid, pbias);
 }
 
-template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0>
+template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0, int NW = 4>
 void launch_rsf(const RsArgs& g, hipStream_t st) {
-  constexpr int smem = 3 * RsGeo<BM, BN, WGM, D, M32>::STAGE;
+  constexpr int smem = 3 * RsGeo<BM, BN, WGM, D, M32, NW>::STAGE;
   static_assert(smem <= 163840, "LDS budget");
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_rsf_kernel<BM, BN, WGM, D, M32, DBG>,
+    (void)hipFuncSetAttribute((const void*)gemm_rsf_kernel<BM, BN, WGM, D, M32, DBG, NW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int tiles = (g.M / BM) * (g.N / BN);
-  hipLaunchKernelGGL((gemm_rsf_kernel<BM, BN, WGM, D, M32, DBG>), dim3(tiles), dim3(256), smem, st, g);
+  hipLaunchKernelGGL((gemm_rsf_kernel<BM, BN, WGM, D, M32, DBG, NW>), dim3(tiles), dim3(64 * NW), smem, st, g);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -1214,7 +1216,16 @@ constexpr RsCfg kRsCfgs[] = {{128, 64, 2, 2, false}, {128, 64, 2, 4, false}, {12
                              {128, 192, 0, 4, true, 4, true, 4},
                              // 59-61: cfgs 35 / 34 / 36 with the fragment sets kept apart (DBG 128)
                              {128, 256, 2, 2, true, 0, false, 3}, {128, 64, 2, 4, true, 0, false, 3},
-                             {128, 192, 2, 2, false, 0, false, 3}};
+                             {128, 192, 2, 2, false, 0, false, 3},
+                             // 62-66: fenced kernel with 8 waves (2 per SIMD: one wave's memory issue overlaps the
+                             // other's MFMAs): 128 x 256 as 2 x 4 / 4 x 2 waves, 128 x 192 (16x16), 128 x 64 (32x32 /
+                             // 16x16, 4 x 2 waves)
+                             {128, 256, 2, 2, true, 0, false, 3}, {128, 256, 4, 2, true, 0, false, 3},
+                             {128, 192, 2, 2, false, 0, false, 3}, {128, 64, 4, 4, true, 0, false, 3},
+                             {128, 64, 4, 4, false, 0, false, 3},
+                             // 67-69: 8-wave kernels at other depths: 128 x 256 D 4, 128 x 192 D 4, 128 x 64 D 2
+                             {128, 256, 2, 4, true, 0, false, 3}, {128, 192, 2, 4, false, 0, false, 3},
+                             {128, 64, 4, 2, true, 0, false, 3}};
 constexpr int kRsNumCfgs = sizeof(kRsCfgs) / sizeof(kRsCfgs[0]);
 
 void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
@@ -1280,7 +1291,15 @@ void launch_rs_cfg(int cfg, const RsArgs& g, hipStream_t st) {
     case 58: launch_rsg<128, 192, true, 4>(g, st); break;
     case 59: launch_rsf<128, 256, 2, 2, true, 128>(g, st); break;
     case 60: launch_rsf<128, 64, 2, 4, true, 128>(g, st); break;
-    default: launch_rsf<128, 192, 2, 2, false, 128>(g, st); break;
+    case 61: launch_rsf<128, 192, 2, 2, false, 128>(g, st); break;
+    case 62: launch_rsf<128, 256, 2, 2, true, 0, 8>(g, st); break;
+    case 63: launch_rsf<128, 256, 4, 2, true, 0, 8>(g, st); break;
+    case 64: launch_rsf<128, 192, 2, 2, false, 0, 8>(g, st); break;
+    case 65: launch_rsf<128, 64, 4, 4, true, 0, 8>(g, st); break;
+    case 66: launch_rsf<128, 64, 4, 4, false, 0, 8>(g, st); break;
+    case 67: launch_rsf<128, 256, 2, 4, true, 0, 8>(g, st); break;
+    case 68: launch_rsf<128, 192, 2, 4, false, 0, 8>(g, st); break;
+    default: launch_rsf<128, 64, 4, 2, true, 0, 8>(g, st); break;
   }
 }
 

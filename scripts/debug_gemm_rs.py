@@ -16,7 +16,9 @@ TILE = {0: (128, 64), 1: (128, 64), 2: (128, 64), 3: (128, 256), 4: (128, 256), 
         29: (128, 256), 30: (128, 192), 31: (128, 128), 32: (128, 64), 33: (128, 64), 34: (128, 64),
         35: (128, 256), 36: (128, 192), 37: (128, 128), 43: (128, 256), 49: (128, 64), 50: (128, 64), 51: (128, 64),
         52: (128, 64), 53: (128, 64), 54: (128, 64), 55: (128, 256), 56: (128, 256), 57: (128, 192), 58: (128, 192),
-        59: (128, 256), 60: (128, 64), 61: (128, 192)}
+        59: (128, 256), 60: (128, 64), 61: (128, 192),
+        62: (128, 256), 63: (128, 256), 64: (128, 192), 65: (128, 64), 66: (128, 64),
+        67: (128, 256), 68: (128, 192), 69: (128, 64)}
 C = ext()
 REPS = int(os.environ.get("REPS", "10"))
 torch.manual_seed(0)
