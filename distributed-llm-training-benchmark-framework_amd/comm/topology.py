@@ -66,7 +66,8 @@ def load_profile(path: str = None):
 
 def fit_alpha_beta(rows, op: str, world: int):
     """Least-squares fit time_us = alpha + bytes * ring_factor / (bus_GBps * 1e3) over the measured
-    sizes of ``op``; returns (alpha_us, bus_GBps) or None (fewer than 2 sizes, non-physical fit)."""
+    sizes of ``op``; returns (alpha_us, bus_GBps) or None (fewer than 2 sizes).  A fit with a non-positive
+    slope (noisy timings) falls back to the largest size as pure bandwidth."""
     from .collectives import ring_factor
     pts = [(float(r["bytes"]), float(r["time_us"])) for r in rows if r.get("op") == op]
     if len(pts) < 2:
@@ -80,8 +81,15 @@ def fit_alpha_beta(rows, op: str, world: int):
     slope = sum((x - mx) * (y - my) for x, y in pts) / sxx        # us per byte
     alpha = my - slope * mx
     f = ring_factor(op, world)
-    if slope <= 0 or f <= 0:
+    if f <= 0:
         return None
+    if slope <= 0:
+        # timings that fall with size (noise: a loaded host, a gloo run beside other jobs): no line
+        # fits, so take the largest message as pure bandwidth -- a conservative bus rate, alpha 1 us
+        xb, yb = max(pts)
+        if yb <= 0:
+            return None
+        slope, alpha = yb / xb, 1.0
     return max(alpha, 1.0), f / (slope * 1e3)
 
 

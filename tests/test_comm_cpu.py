@@ -123,6 +123,10 @@ def test_alpha_beta_fit_and_measured_bucket(tmp_path, monkeypatch):
     assert recommend_bucket_mb(8) == 64.0
     monkeypatch.setenv("DLTB_XGMI_PROFILE", str(tmp_path / "missing.json"))
     assert measured_params(8)[2] == "default"
+    # noisy timings that fall with size: the largest message as pure bandwidth, alpha 1 us
+    noisy = [{"op": "all_gather", "bytes": 4 << 20, "time_us": 300.0}, {"op": "all_gather", "bytes": 16 << 20, "time_us": 200.0}]
+    a, g = fit_alpha_beta(noisy, "all_gather", world)
+    assert a == 1.0 and abs(g - ring_factor("all_gather", world) * (16 << 20) / 200.0 / 1e3) < 1e-9
 
 
 def _calib_worker(rank, world, port, out_path):
