@@ -391,7 +391,11 @@ def _own_nt(a, b_nk, bias=None):
     """a [M, K] @ b_nk[N, K]^T (+ bias) through gemm_rs when the table holds the shape, else None."""
     global own_gemm_calls
     if not (a.is_cuda and a.dtype == torch.bfloat16 and b_nk.dtype == torch.bfloat16 and a.dim() == 2
-            and a.stride(1) == 1 and b_nk.stride(1) == 1 and a.stride(0) % 8 == 0 and b_nk.stride(0) % 8 == 0):
+            and a.stride(1) == 1 and b_nk.stride(1) == 1 and a.stride(0) % 8 == 0 and b_nk.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b_nk.data_ptr() % 16 == 0):      # 16-byte operand loads
+        return None
+    if bias is not None and not (bias.dtype == torch.bfloat16 and bias.is_contiguous()
+                                 and bias.data_ptr() % 8 == 0):               # 8-byte bias loads
         return None
     M, K = a.shape
     N = b_nk.shape[0]
