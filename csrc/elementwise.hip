@@ -30,6 +30,26 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
+// g = GELU(f) and gp = GELU'(f) in one pass (the erf and exp of the derivative are the forward's own): the
+// backward's dGELU then rides in the fc2 data-gradient GEMM's epilogue (gemm_rs aux) and f is not kept.
+__global__ __launch_bounds__(256) void gelu_fwd_grad_kernel(const bf16_t* __restrict__ f, bf16_t* __restrict__ g,
+                                                           bf16_t* __restrict__ gp, long n8) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float v[8], d[8];
+    unpack8(ld16<uint4>(f + i * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float ex;                                          // exp(-x^2 / 2)
+      const float x = v[e];
+      const float cdf = 0.5f * (1.f + erf_fast(x * 0.70710678118654752f, &ex));
+      v[e] = x * cdf;
+      d[e] = cdf + x * 0.39894228040143268f * ex;
+    }
+    *reinterpret_cast<uint4*>(g + i * 8) = pack8(v);
+    *reinterpret_cast<uint4*>(gp + i * 8) = pack8(d);
+  }
+}
+
 // Column-partials layout shared by gelu_bwd_colsum and colsum:
 //   block (bx, by): columns [bx*512, bx*512+512), rows [by*rps, (by+1)*rps)
 //   thread: lane = tid & 63 -> 8 columns, phase = tid >> 6 -> every 4th row
@@ -320,6 +340,12 @@ void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st) {
   const long n8 = n / 8;
   hipLaunchKernelGGL(gelu_fwd_kernel, dim3(ew_grid(n8)), dim3(256), 0, st, (const bf16_t*)f,
                      (bf16_t*)g, n8);
+}
+
+void dltb_gelu_fwd_grad(const void* f, void* g, void* gp, long n, hipStream_t st) {
+  const long n8 = n / 8;
+  hipLaunchKernelGGL(gelu_fwd_grad_kernel, dim3(ew_grid(n8)), dim3(256), 0, st, (const bf16_t*)f, (bf16_t*)g,
+                     (bf16_t*)gp, n8);
 }
 
 int dltb_colsum_partials(int N) { return colsum_splits(N); }

@@ -46,6 +46,10 @@ struct RsArgs {
   int M, N, K;
   int gm;            // m-tiles per group of the XCD-aware walk
   int accumulate;
+  // fp32-image kernels only: C = (A B^T) * aux elementwise (aux [M, N] bf16, row stride ldc), rounded once, and
+  // part[m-tile][n] = the column sums of the rounded C over the tile's rows (the dGELU epilogue: aux = GELU'(f))
+  const bf16_t* aux;
+  float* part;
 };
 
 DLTB_DEV f32x4 mfma16(rs_frag a, rs_frag b, f32x4 c) {
@@ -127,11 +131,32 @@ struct RsEpiF {
   DLTB_DEV static void put(uint32_t lds0, int ml, int nl, const float* a) {
     *(lds_f4t*)(size_t)(lds0 + (ml * P + nl) * 4) = f32x4{a[0], a[1], a[2], a[3]};
   }
-  DLTB_DEV static void flush(const RsArgs& g, uint32_t lds0, int m0, int n0, int tid, const Bias& pb) {
+  // the aux values of this thread's epilogue chunks, loaded at kernel start (the aux operand is cold: its
+  // loads issued in the epilogue exposed their HBM latency row after row)
+  static constexpr int ITER = BM * CPR / NT;
+  static constexpr bool AUX_PF = ITER <= 16;            // <= 32 VGPRs held through the k-loop
+  struct Aux {
+    uint2 v[AUX_PF ? ITER : 1];
+  };
+  DLTB_DEV static void prefetch_aux(const RsArgs& g, int m0, int n0, int tid, Aux& ax) {
+    if constexpr (AUX_PF) {
+      if (g.aux) {
+#pragma unroll
+        for (int i = 0; i < ITER; ++i) {
+          const int c = tid + i * NT, row = c / CPR, ch = c - row * CPR;
+          ax.v[i] = *reinterpret_cast<const uint2*>(g.aux + (size_t)(m0 + row) * g.ldc + n0 + ch * 4);
+        }
+      }
+    }
+  }
+  DLTB_DEV static void flush(const RsArgs& g, uint32_t lds0, int m0, int n0, int tid, const Bias& pb,
+                             const Aux& ax = Aux{}) {
     constexpr int CHUNKS = BM * CPR;
     static_assert(CHUNKS % NT == 0, "epilogue chunks");
-#pragma unroll 8
-    for (int c = tid; c < CHUNKS; c += NT) {
+    float cs[4] = {0.f, 0.f, 0.f, 0.f};                // dGELU epilogue: this thread's column sums
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {                   // fully unrolled: ax.v[i] stays in registers
+      const int c = tid + i * NT;
       const int row = c / CPR, ch = c - row * CPR;
       const f32x4 x = *(lds_f4t*)(size_t)(lds0 + (row * P + ch * 4) * 4);
       float v[4] = {x[0], x[1], x[2], x[3]};
@@ -141,15 +166,39 @@ struct RsEpiF {
         const uint2 bb = *reinterpret_cast<const uint2*>(g.bias + n0 + ch * 4);
         v[0] += lo_bf(bb.x); v[1] += hi_bf(bb.x); v[2] += lo_bf(bb.y); v[3] += hi_bf(bb.y);
       }
-      bf16_t* dst = g.c + (size_t)(m0 + row) * g.ldc + n0 + ch * 4;
+      const size_t off = (size_t)(m0 + row) * g.ldc + n0 + ch * 4;
+      bf16_t* dst = g.c + off;
       if (g.accumulate) {
         const uint2 old = *reinterpret_cast<const uint2*>(dst);
         v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+      }
+      if (g.aux) {
+        uint2 a2;
+        if constexpr (AUX_PF) a2 = ax.v[i];
+        else a2 = *reinterpret_cast<const uint2*>(g.aux + off);
+        v[0] *= lo_bf(a2.x); v[1] *= hi_bf(a2.x); v[2] *= lo_bf(a2.y); v[3] *= hi_bf(a2.y);
       }
       uint2 o;
       o.x = pack_bf2(v[0], v[1]);
       o.y = pack_bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(dst) = o;
+      if (g.part) {                                    // sum the rounded values the next GEMM reads
+        cs[0] += lo_bf(o.x); cs[1] += hi_bf(o.x); cs[2] += lo_bf(o.y); cs[3] += hi_bf(o.y);
+      }
+    }
+    if (FIXED && g.part) {
+      // threads t, t + CPR, ... hold the same 4 columns: fold them through LDS (the image is free once
+      // every thread has stored its rows), one partial row per m-tile
+      constexpr int G = NT / CPR;
+      __syncthreads();
+      *(lds_f4t*)(size_t)(lds0 + tid * 16) = f32x4{cs[0], cs[1], cs[2], cs[3]};
+      __syncthreads();
+      if (tid < CPR) {
+        f32x4 t = *(lds_f4t*)(size_t)(lds0 + tid * 16);
+#pragma unroll
+        for (int j = 1; j < G; ++j) t += *(lds_f4t*)(size_t)(lds0 + (tid + j * CPR) * 16);
+        *reinterpret_cast<float4*>(g.part + (size_t)(m0 / BM) * g.N + n0 + tid * 4) = make_float4(t[0], t[1], t[2], t[3]);
+      }
     }
   }
 };
@@ -612,6 +661,8 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_rsf_kernel(RsArgs g) {
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
   using E = RsEpiF<BM, BN, 64 * NW>;
   const typename E::Bias pbias = E::prefetch(g.bias, n0, tid);
+  typename E::Aux paux;
+  E::prefetch_aux(g, m0, n0, tid, paux);
 
   constexpr int RL = M32 ? 32 : 16;
   const int fr = lane & (RL - 1), fq = M32 ? (lane >> 5) : (lane >> 4);
@@ -754,7 +805,7 @@ __global__ __launch_bounds__(64 * NW, 1) void gemm_rsf_kernel(RsArgs g) {
     }
   }
   rs_barrier();
-  E::flush(g, lds0, m0, n0, tid, pbias);
+  E::flush(g, lds0, m0, n0, tid, pbias, paux);
 }
 
 template <int BM, int BN, int WGM, int D, bool M32, int DBG = 0, int NW = 4>
@@ -1333,8 +1384,18 @@ bool dltb_gemm_rs_supported(int M, int N, int K, int cfg) {
   return rs_fits(cfg, M, N, K);
 }
 
+int dltb_gemm_rs_bm(int cfg) { return (cfg >= 0 && cfg < kRsNumCfgs) ? kRsCfgs[cfg].bm : 0; }
+
+bool dltb_gemm_rs_aux_supported(int M, int N, int K, int cfg) {
+  // the aux / column-partial epilogue: fp32-image kernels (kinds 3), a thread's columns fixed across rows
+  if (!dltb_gemm_rs_supported(M, N, K, cfg) || kRsCfgs[cfg].kind != 3) return false;
+  const int nt = (cfg >= 62 && cfg <= 69) ? 512 : 256;
+  const int cpr = kRsCfgs[cfg].bn / 4;
+  return nt % cpr == 0 && kRsCfgs[cfg].bm * cpr / nt <= 16;   // the aux values prefetched (RsEpiF::AUX_PF)
+}
+
 int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st) {
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, const void* aux, float* part) {
   if (cfg < 0) cfg = dltb_gemm_rs_pick(M, N, K);
   if (!dltb_gemm_rs_supported(M, N, K, cfg)) return -1;
   RsArgs g{};
@@ -1350,6 +1411,9 @@ int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long l
   g.K = K;
   g.gm = gm;
   g.accumulate = accumulate;
+  g.aux = (const bf16_t*)aux;
+  g.part = part;
+  if ((aux || part) && !dltb_gemm_rs_aux_supported(M, N, K, cfg)) return -1;
   launch_rs_cfg(cfg, g, st);
   return cfg;
 }

@@ -38,6 +38,7 @@ bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const flo
 
 // elementwise.hip
 void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st);
+void dltb_gelu_fwd_grad(const void* f, void* g, void* gp, long n, hipStream_t st);   // g = GELU(f), gp = GELU'(f)
 int dltb_colsum_partials(int N);
 void dltb_gelu_bwd(const void* dg, const void* f, void* df, float* part, void* db, int accumulate,
                    int N, int k, hipStream_t st);
@@ -164,7 +165,11 @@ int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long l
 int dltb_gemm_rs_pick(int M, int N, int K);
 bool dltb_gemm_rs_supported(int M, int N, int K, int cfg);
 int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st);
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, const void* aux = nullptr,
+                 float* part = nullptr);
+int dltb_gemm_rs_bm(int cfg);
+// C = (A B^T) * aux (elementwise, rounded once) with per-m-tile fp32 column partials of C (the dGELU epilogue)
+bool dltb_gemm_rs_aux_supported(int M, int N, int K, int cfg);
 
 // device-scalar helpers (head backward: no host sync)
 void dltb_xent_mean(const float* loss, const int64_t* targets, int N, int64_t ignore_index, float* out,

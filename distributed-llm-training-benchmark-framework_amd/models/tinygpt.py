@@ -145,12 +145,18 @@ class _BlockFn(torch.autograd.Function):
         else:
             x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
         f = F_.linear_fwd(h2, w1, b1)
-        g = F_.gelu_fwd(f, out=lb and lb.g)
+        # dGELU-epilogue path (own-GEMM table): keep GELU'(f) for the backward instead of f
+        dgelu = f.is_cuda and F_.dgelu_fused(f.shape[0], f.shape[1], w2.shape[0])
+        if dgelu:
+            g, f = F_.gelu_fwd_grad(f, out=lb and lb.g)
+        else:
+            g = F_.gelu_fwd(f, out=lb and lb.g)
         m = F_.linear_fwd_splitk(g, w2, b2) if model.splitk_planes else None
         if m is None:
             m = F_.linear_fwd(g, w2, b2)    # Dropout(m) + x1 happens in the consumer's LayerNorm
         rt.release_forward(unit)
         ctx.model, ctx.i, ctx.lb = model, i, lb
+        ctx.dgelu = dgelu                   # saved f is GELU'(f): the backward takes the dGELU-epilogue GEMM
         ctx.fused_prev = m_in is not None   # LN1 applied the previous block's MLP dropout
         ctx.saved = (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g)
         return x1, m
@@ -187,8 +193,14 @@ class _BlockFn(torch.autograd.Function):
         dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
                                  out=lb and lb.dm)
         wgrad(10, dm, g, ("dm", "g"))
-        dg = F_.linear_dgrad(dm, w2, rt.weight_t(unit, 10, w2))
-        df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
+        w2t = rt.weight_t(unit, 10, w2)
+        df = None
+        if ctx.dgelu:                   # f holds GELU'(f): dGELU and the fc1 bias partials in the GEMM epilogue
+            df = F_.linear_dgrad_dgelu(dm, w2t, f, s[9][0], s[9][1], red, out=lb and lb.df)
+            assert df is not None, "dGELU epilogue planned in the forward but unavailable in the backward"
+        else:
+            dg = F_.linear_dgrad(dm, w2, w2t)
+            df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
         wgrad(8, df, h2, ("df", "h2"))
         w1t = rt.weight_t(unit, 8, w1)
         dh2 = F_.linear_dgrad_splitk(df, w1t) if model.splitk_planes else None

@@ -204,6 +204,36 @@ def gelu_fwd(f, out=None):
     return ext().gelu_fwd(f, out) if _gpu(f) else _into(out, ref.gelu_fwd(f))
 
 
+def gelu_fwd_grad(f, out=None, gp_out=None):
+    """(g, gp) = (GELU(f), GELU'(f)) in one pass (GPU): the forward of the dGELU-epilogue path."""
+    return tuple(ext().gelu_fwd_grad(f, out, gp_out))
+
+
+# dGELU in the fc2 data gradient's epilogue: own-GEMM table rows with bias = 2 (``gemm_rs_aux``)
+_DGELU = 2
+
+
+def dgelu_fused(M, N, K):
+    """True when the fc2 data gradient (M tokens, N = the MLP width, K = the model width) runs with the dGELU
+    epilogue: the forward then keeps GELU'(f) instead of f (models/tinygpt.py)."""
+    return (M, N, K, _DGELU) in rs_table()
+
+
+def linear_dgrad_dgelu(dy2d, wt, gp, db, accumulate, red, out=None):
+    """df = (dY W) * GELU'(f) with the fc1 bias gradient's column partials, one own-GEMM launch
+    (C = dY (W^T)^T; the epilogue multiplies by gp = GELU'(f) from the forward, rounds once and sums the rounded
+    columns per 128-row tile; the partials are reduced at ``red.flush()``).  None when the table has no row."""
+    global own_gemm_calls
+    M, K = dy2d.shape
+    hit = rs_table().get((M, wt.shape[0], K, _DGELU))
+    if hit is None or red is None:
+        return None
+    own_gemm_calls += 1
+    df, part = ext().gemm_rs_aux(dy2d, wt, out, gp, hit[0], hit[1])
+    red.add(part, db, accumulate)
+    return df
+
+
 def gelu_bwd(dg, f, db, accumulate, red=None, out=None):
     """df = dg * gelu'(f); the fc1 bias gradient colsum(df) is fused (reduced at red.flush())."""
     if _gpu(dg):

@@ -80,3 +80,33 @@ def test_model_step_issues_own_gemm():
     torch.cuda.synchronize()
     assert F.own_gemm_calls - c0 == len(_rows()), "every shipped product should run on the own kernel"
     assert 5.0 < float(loss.item()) < 15.0
+
+
+@pytest.mark.parametrize("cfg", [62])
+def test_dgelu_epilogue(cfg):
+    """gemm_rs_aux: out = (a b^T) * aux rounded once, part = per-128-row column sums of the rounded out --
+    the fc2 data gradient with the GELU backward and the fc1 bias partials fused (aux = GELU'(f))."""
+    C = ext()
+    M, N, K = 2048, 4096, 1024
+    assert C.gemm_rs_aux_supported(M, N, K, cfg)
+    assert not C.gemm_rs_aux_supported(M, N, K, 35)      # 4 waves: 32 aux chunks per thread, not prefetched
+    torch.manual_seed(cfg)
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    f = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    g, gp = C.gelu_fwd_grad(f)
+    x = f.float()
+    ref_g = torch.nn.functional.gelu(x)
+    cdf = 0.5 * (1 + torch.erf(x / 2 ** 0.5))
+    ref_gp = cdf + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    assert (g.float() - ref_g).abs().max().item() <= 2e-2 * ref_g.abs().max().item()
+    assert (gp.float() - ref_gp).abs().max().item() <= 1e-2
+    out, part = C.gemm_rs_aux(a, b, None, gp, cfg, 4)
+    torch.cuda.synchronize()
+    ref = (a.float() @ b.float().t()) * gp.float()
+    tol = ref.abs().max().item() * 2 ** -7 + 1e-2
+    assert (out.float() - ref).abs().max().item() <= tol
+    assert part.shape == (M // 128, N)
+    # the partials sum the ROUNDED outputs, per 128-row tile
+    ref_part = out.float().view(M // 128, 128, N).sum(1)
+    assert torch.allclose(part, ref_part, rtol=1e-4, atol=1e-3)
