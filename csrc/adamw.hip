@@ -132,15 +132,19 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
     const G* __restrict__ grad, const int* __restrict__ blk_seg, const int64_t* __restrict__ blk_start,
     const int64_t* __restrict__ seg_ostart, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, const float* __restrict__ hp,
-    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int wide_ab) {
+    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int wide_ab,
+    int nblk) {
   if (hp) {   // step-dependent hyper-parameters from device memory (HIP-graph replays)
     if (hp[3] != 0.f) return;   // dynamic loss scaling found an inf / nan: the step is skipped
     lr = hp[0];
     step_size = hp[1];
     inv_sqrt_bc2 = hp[2];
   }
-  const int seg = blk_seg[blockIdx.x];
-  const int64_t start = blk_start[blockIdx.x];
+  // one table row per block, or (a grid capped below the row count: DDP's early per-bucket updates
+  // trickling beside the backward on a side stream) a block-strided walk over the rows
+  for (int bi = blockIdx.x; bi < nblk; bi += gridDim.x) {
+  const int seg = blk_seg[bi];
+  const int64_t start = blk_start[bi];
   const int64_t s0 = seg_ostart[seg];
   const int64_t seg_end = s0 + seg_len[seg];
   DLTB_DCHECK(seg >= 0 && start >= s0 && start < seg_end);
@@ -158,6 +162,7 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
   else if (blockDim.x == kAdamThreads / 2)   // A/B (DLTB_ADAM_T128=1): half the lanes, twice the loads in flight each
     adamw_block<G, 4, kAdamThreads / 2>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
   else adamw_block<G, 4>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
+  }
 }
 
 // sum of squares in a FIXED order (bitwise reproducible: eager runs, graph replays and ranks agree):
@@ -266,18 +271,19 @@ void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* gr
                 const int* blk_seg, const int64_t* blk_start, int nblocks, const int64_t* seg_ostart,
                 const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, const float* hp,
                 float lr, float beta1, float beta2, float eps, float wd, float step_size,
-                float inv_sqrt_bc2, hipStream_t st) {
+                float inv_sqrt_bc2, int grid_cap, hipStream_t st) {
   if (nblocks <= 0) return;
+  const int grid = grid_cap > 0 && grid_cap < nblocks ? grid_cap : nblocks;
   static const int wide = getenv("DLTB_ADAM_WIDE") ? atoi(getenv("DLTB_ADAM_WIDE")) : 0;   // A/B: 16-byte path
   static const int thr = getenv("DLTB_ADAM_T128") && atoi(getenv("DLTB_ADAM_T128")) ? kAdamThreads / 2 : kAdamThreads;
   if (grad_bf16)
-    hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(nblocks), dim3(thr), 0, st, master,
+    hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(grid), dim3(thr), 0, st, master,
                        exp_avg, exp_avg_sq, (const bf16_t*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide, nblocks);
   else
-    hipLaunchKernelGGL(adamw_kernel<float>, dim3(nblocks), dim3(thr), 0, st, master,
+    hipLaunchKernelGGL(adamw_kernel<float>, dim3(grid), dim3(thr), 0, st, master,
                        exp_avg, exp_avg_sq, (const float*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide, nblocks);
 }
 
 int dltb_sumsq_partials() { return kSumsqBlocks; }

@@ -86,7 +86,7 @@ void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* gr
                 const int* blk_seg, const int64_t* blk_start, int nblocks, const int64_t* seg_ostart,
                 const int64_t* seg_len, const int64_t* seg_dst, const float* gscale, const float* hp,
                 float lr, float beta1, float beta2, float eps, float wd, float step_size,
-                float inv_sqrt_bc2, hipStream_t st);
+                float inv_sqrt_bc2, int grid_cap, hipStream_t st);   // grid_cap 0: one block per row
 int dltb_sumsq_partials();
 void dltb_sumsq(const void* x, bool bf16, long n, float* out, float* part, hipStream_t st);
 void dltb_clip_coef(const float* norm_sq, float max_norm, float* coef, float* norm_out,

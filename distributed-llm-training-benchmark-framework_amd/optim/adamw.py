@@ -107,17 +107,19 @@ class FlatAdamW:
     def launches_per_step(self) -> int:
         return len(self._sub_ranges) if self._sub_ranges else 1
 
-    def _launch_rows(self, lo, hi, grad, gscale):
+    def _launch_rows(self, lo, hi, grad, gscale, grid_cap=0):
         b1, b2 = self.betas
         ext().adamw(self.master, self.exp_avg, self.exp_avg_sq, grad, self._tables[0][lo:hi],
                     self._tables[1][lo:hi], *self._tables[2:], gscale,
-                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16)
+                    self._lr_now, b1, b2, self.eps, self.weight_decay, self.step_count, self.hp, self.dst_f16,
+                    grid_cap)
 
-    def launch_segment(self, i: int, grad: torch.Tensor, gscale: torch.Tensor = None):
+    def launch_segment(self, i: int, grad: torch.Tensor, gscale: torch.Tensor = None, grid_cap: int = 0):
         """The update of segment ``i`` alone (one launch over a slice of the block tables; the
         blocks of a segment are contiguous rows).  With ``prepare`` called once per step, the
         per-segment launches together are exactly ``launch`` -- the engine uses them to let each
-        bucket's forward wait for its own parameters only."""
+        bucket's forward wait for its own parameters only.  ``grid_cap`` > 0 runs the rows on at most
+        that many workgroups (a side-stream update that should leave the CUs to concurrent kernels)."""
         if not self.master.is_cuda:              # CPU reference: the same update on the segment's rows
             b1, b2 = self.betas
             ostart, length, dst = self.segments[i]
@@ -127,7 +129,7 @@ class FlatAdamW:
             dst.copy_(self.master[sl])
             return
         lo, hi = self._seg_blocks[i]
-        self._launch_rows(lo, hi, grad, gscale)
+        self._launch_rows(lo, hi, grad, gscale, grid_cap)
 
     @torch.no_grad()
     def step(self, grad: torch.Tensor, lr: float, gscale: torch.Tensor = None):

@@ -156,6 +156,21 @@ class ReplicatedEngine(Engine):
         # norm: both keep the whole-model update after the last wait.)
         self._ddp_pipe = self._ddp_pipe_wanted()
         self._ar_works = {}      # bucket -> its all-reduce (untracked) while the pipeline is on
+        # A/B (DLTB_DDP_EARLY_OPT=1; off by default): at world > 1 on the GPU, a bucket's AdamW segment
+        # runs on a side stream as soon as its all-reduce lands, i.e. under the rest of the backward
+        # instead of after it.  A reduced bucket's parameters are not read again by this backward (its
+        # blocks' dgrad / dW ran before the all-reduce was issued); the next forward waits for the side
+        # stream; the tied token table's bucket stays last (its gathered rows).  Measured slower: the
+        # emulated ddp_bf16 N = 8 step 10.07 -> 10.25 ms with full grids, 10.27 / 10.69 / 12.5 ms with
+        # the update capped at 128 / 64 / 32 workgroups (profiles/ddp_early_update_ab_r5.txt) -- the
+        # backward's kernels lose more to the co-running update than the tail gains.
+        self._early_opt = (self._ddp_pipe and self.device.type == "cuda"
+                           and os.environ.get("DLTB_DDP_EARLY_OPT", "0") == "1")
+        self._opt_stream = torch.cuda.Stream(self.device) if self._early_opt else None
+        # workgroups of each early update (0: one per table row): a capped grid leaves the CUs to the
+        # backward's kernels and trickles the update beside them
+        self._early_grid = int(os.environ.get("DLTB_DDP_EARLY_GRID", 0))
+        self._early = None       # this step's early-update state: {"done": set, "gscale": t} or None
         if self._ddp_pipe:
             g_full = self.comm_f32 if self.comm_f32 is not None else self.flat_grad
             opt_segs = [(bk.start, bk.end - bk.start, self.flat_param[bk.start:bk.end]) for bk in L.buckets]
@@ -379,6 +394,8 @@ class ReplicatedEngine(Engine):
                 g = c
             if self._ddp_pipe:       # waited by its own AdamW segment (or the token rows), not wait_all
                 self._ar_works[b] = self.comm.all_reduce(g, async_op=True, track=False)
+                if self._early_opt and self._is_boundary:
+                    self._launch_early(b)
             else:
                 self.comm.all_reduce(g, async_op=not sync)
         elif not self._use_rs:
@@ -492,6 +509,32 @@ class ReplicatedEngine(Engine):
                 and self.scaler is None and not cfg.grad_clip > 0 and not cfg.extra.get("track_grad_norm", False)
                 and os.environ.get("DLTB_DDP_OPT_PIPELINE", "1") == "1")
 
+    def _tied_bucket(self):
+        tu = getattr(self.model, "tok_slot", (None,))[0]
+        return self._bucket_of.get(id(tu)) if tu is not None else None
+
+    def _launch_early(self, b):
+        """AdamW of bucket ``b`` on the side stream, behind its all-reduce (see ``_early_opt``)."""
+        from ..comm.collectives import _EmuWork
+        w = self._ar_works.get(b)
+        if b == self._tied_bucket() or w is None:
+            return
+        if not (isinstance(w, _EmuWork) or type(w).__module__.startswith("torch")):
+            return                               # lazy / host-staged works run their copies at wait()
+        if self._early is None:                  # first early bucket of this step: lr, hp, coefficient
+            g = self._owner_grad()
+            self.opt.prepare(self.sched(self.opt_steps))
+            gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._early = {"done": set(), "gscale": gscale, "ev": ev}
+        g = self._owner_grad()
+        with torch.cuda.stream(self._opt_stream):
+            self._opt_stream.wait_event(self._early["ev"])
+            self._ar_works.pop(b).wait()         # this stream waits for the all-reduce
+            self.opt.launch_segment(b, g, self._early["gscale"], grid_cap=self._early_grid)
+        self._early["done"].add(b)
+
     def _wait_allreduce(self, b):
         w = self._ar_works.pop(b, None)
         if w is not None:
@@ -503,18 +546,26 @@ class ReplicatedEngine(Engine):
             # the tied token table's bucket goes last: its gathered token rows (issued after every
             # all-reduce) are scatter-added into it first
             g = self._owner_grad()
-            gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)   # (no clip: a fill)
-            self.opt.prepare(lr)
+            early, self._early = self._early, None
+            if early is None:
+                gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)   # (no clip: a fill)
+                self.opt.prepare(lr)
+            else:                                # lr / hp / coefficient already set by _launch_early
+                gscale = early["gscale"]
             order = list(range(len(self.layout.buckets)))
             bt = self._bucket_of[id(self._sparse[0][0])] if self._sparse is not None else None
             if bt is not None:
                 order.remove(bt)
                 order.append(bt)
             for b in order:
+                if early is not None and b in early["done"]:
+                    continue
                 self._wait_allreduce(b)
                 if b == bt:
                     self._apply_sparse()
                 self.opt.launch_segment(b, g, gscale)
+            if early is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
             return
         self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
 

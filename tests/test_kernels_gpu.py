@@ -544,6 +544,26 @@ def test_adamw_mixed_alignment_segments():
     close(out_bf16, tp.detach().to(torch.bfloat16), 1e-2, 1e-2, "adamw bf16 copy (two segments)")
 
 
+def test_adamw_grid_cap_bitwise():
+    """A capped grid (DDP's side-stream early update, DLTB_DDP_EARLY_GRID) walks the block table
+    block-strided: bitwise the one-block-per-row launch."""
+    C = ext()
+    n = 300_000
+    p0 = torch.randn(n, device=DEV)
+    outs = []
+    for cap in (0, 7):
+        master, m, v = p0.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+        out_bf16 = torch.empty(n, device=DEV, dtype=torch.bfloat16)
+        tabs = _adam_tables(n, out_bf16, C.adamw_chunk())
+        assert tabs[0].numel() > 7
+        for step in range(1, 3):
+            g = torch.randn(n, device=DEV, generator=torch.Generator(DEV).manual_seed(step)).to(torch.bfloat16)
+            C.adamw(master, m, v, g, *tabs, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, None, False, cap)
+        outs.append((master, m, v, out_bf16))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_sumsq_clip():
     C = ext()
     x = torch.randn(1 << 20, device=DEV)
