@@ -184,6 +184,15 @@ class ReplicatedEngine(Engine):
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
         self._wq = WgradQueue()
+        # A/B (DLTB_WGRAD_SIDE = G blocks, 0 = off): at world 1 the window's batched dW of every G
+        # blocks whose backward has finished is issued on a side stream, beside the rest of the dX
+        # chain (whose per-layer GEMMs run one tile per CU and leave MFMA idle), instead of all 16
+        # blocks after it; the main stream joins the side stream at the end of the backward
+        self._side_group = int(os.environ.get("DLTB_WGRAD_SIDE", 0)) if (
+            self.world == 1 and dev.type == "cuda" and self.defer_wgrad) else 0
+        self._wgrad_stream = torch.cuda.Stream(dev) if self._side_group > 0 else None
+        self._side_units = []    # reported units whose queued dW waits for a side-stream batch
+        self._side_hold = []     # their operands, alive until the join (the main stream may free them)
         # Window-wide weight gradients: where no collective reads a gradient before the window ends
         # (world 1, or the window-reduced ZeRO-1 / DDP paths), the model keeps every micro-step's
         # dW operands and the window's dW = sum_m dY_m^T X_m runs at its last micro-step as one
@@ -278,6 +287,10 @@ class ReplicatedEngine(Engine):
 
     def grads_ready(self, unit):
         self._reported.add(id(unit))
+        if self._side_group and self._wq.has([unit]):
+            self._side_units.append(unit)
+            if len(self._side_units) >= self._side_group:
+                self._side_flush()
         if self._carry is not None and self._carry[0][0] is unit:
             self._apply_carry()
         b = self._bucket_of.get(id(unit))
@@ -455,9 +468,21 @@ class ReplicatedEngine(Engine):
         if self.stage == 2 and self.world > 1:
             self._written.clear()         # the full gradient buffer is reduced every micro-step
 
+    def _side_flush(self):
+        units, self._side_units = self._side_units, []
+        self._side_hold.extend(self._wq.pending(units))
+        self._wgrad_stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._wgrad_stream):
+            self._wq.flush(units)
+
     def _finish_backward(self):
         if self._red is not None:
             self._red.flush()
+        if self._side_hold or self._side_units:
+            self._side_units = []
+            self._wq.flush()                                    # what did not fill a side batch
+            torch.cuda.current_stream(self.device).wait_stream(self._wgrad_stream)
+            self._side_hold = []
         self._wq.flush()                                        # world 1: every block in one batch
         self._zero_unreported()
         if self._reduce_now():

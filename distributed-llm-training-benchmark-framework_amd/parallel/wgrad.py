@@ -66,6 +66,10 @@ class WgradQueue:
         """Whether any of ``units`` has queued products."""
         return any(id(u) in self._items for u in units)
 
+    def pending(self, units) -> list:
+        """The queued items of ``units`` (references that keep their operands alive)."""
+        return [it for u in units for it in self._items.get(id(u), ())]
+
     def __len__(self):
         return sum(len(v) for v in self._items.values())
 
