@@ -76,11 +76,25 @@ def problem(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, accumulate: bool,
             int(bias is not None))
 
 
+def resolve_config_path(path: str, what: str) -> str:
+    """A table path as given, or relative to the repository root when the working directory does
+    not hold it (profilers run bench.py from /tmp).  A named table that exists nowhere is an error:
+    silently running without it would time a different configuration."""
+    if path == "none" or os.path.isabs(path) or os.path.exists(path):
+        if path != "none" and not os.path.exists(path):
+            raise FileNotFoundError(f"{what}: {path} does not exist")
+        return path
+    alt = os.path.join(_ROOT, path)
+    if not os.path.exists(alt):
+        raise FileNotFoundError(f"{what}: {path} exists neither in {os.getcwd()} nor in {_ROOT}")
+    return alt
+
+
 def load(path: str = None, verbose: bool = False) -> int:
     """Read the tuning table (``DLTB_BLASLT_FILE`` or the shipped one); entries whose solution name
     no longer matches the loaded library are dropped.  Returns the number of usable entries."""
     global _enabled
-    path = path or os.environ.get("DLTB_BLASLT_FILE", DEFAULT_FILE)
+    path = resolve_config_path(path or os.environ.get("DLTB_BLASLT_FILE", DEFAULT_FILE), "DLTB_BLASLT_FILE")
     _table.clear()
     _enabled = False
     if not torch.cuda.is_available():

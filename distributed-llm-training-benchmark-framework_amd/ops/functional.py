@@ -410,6 +410,9 @@ def rs_table():
     if _rs_table is None:
         _rs_table = {}
         path = _os.environ.get("DLTB_OWN_GEMM_TABLE", _RS_FILE)
+        if path != _RS_FILE and path != "none":
+            from .blaslt import resolve_config_path
+            path = resolve_config_path(path, "DLTB_OWN_GEMM_TABLE")
         if _os.environ.get("DLTB_OWN_GEMM", "1") == "1" and _os.path.exists(path):
             with open(path) as f:
                 for r in _csv.DictReader(ln for ln in f if not ln.startswith("#")):

@@ -108,3 +108,19 @@ def test_own_gemm_table_parsing(tmp_path, monkeypatch):
     shipped = F.rs_table()
     assert shipped and all(v[0] in (34, 49, 50) for v in shipped.values())
     F._rs_table = None
+
+
+def test_table_paths_resolve_from_any_cwd(tmp_path, monkeypatch):
+    """A relative DLTB_BLASLT_FILE / DLTB_OWN_GEMM_TABLE resolves against the repository root when the
+    working directory does not hold it (rocprofv3 runs bench.py from /tmp); a missing table is an error,
+    not a silent run without it."""
+    import pytest
+    from dltb.ops.blaslt import _ROOT, resolve_config_path
+    monkeypatch.chdir(tmp_path)
+    rel = os.path.join("configs", "blaslt", "blaslt_gfx950.csv")
+    assert resolve_config_path(rel, "t") == os.path.join(_ROOT, rel)
+    assert resolve_config_path("none", "t") == "none"
+    with pytest.raises(FileNotFoundError):
+        resolve_config_path("configs/blaslt/no_such_table.csv", "t")
+    with pytest.raises(FileNotFoundError):
+        resolve_config_path(str(tmp_path / "missing.csv"), "t")
