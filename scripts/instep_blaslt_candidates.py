@@ -32,7 +32,16 @@ PRODUCTS = {
     "qkv.fwd": (1, 0, 3072, 2048, 1024, 1),
     "fc1.fwd": (1, 0, 4096, 2048, 1024, 1),
     "fc2.dgrad": (1, 0, 4096, 2048, 1024, 0),
+    # the N = 1024 products (own gemm_rsf cfg 34 in the shipped step): a candidate table for these
+    # comes with an own-GEMM table lacking the product (<name>_<i>.own.csv, DLTB_OWN_GEMM_TABLE)
+    "out.fwd": (1, 0, 1024, 2048, 1024, 1),
+    "fc2.fwd": (1, 0, 1024, 2048, 4096, 1),
+    "out.dgrad": (1, 0, 1024, 2048, 1024, 0),
+    "fc1.dgrad": (1, 0, 1024, 2048, 4096, 0),
+    "qkv.dgrad": (1, 0, 1024, 2048, 3072, 0),
 }
+OWN_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "gemm_rs",
+                         "gemm_rs_gfx950.csv")
 
 
 def macro_tile(name):
@@ -49,7 +58,10 @@ def main():
     ap.add_argument("--out-dir", default="gpurun_out/blaslt_ab")
     args = ap.parse_args()
     rargs = argparse.Namespace(tier="A", seq_len=2048, strategy="zero2", dtype="bf16", grad_accum=4, emulate=0)
+    os.environ["DLTB_OWN_GEMM"] = "0"       # every product through hipBLASLt while recording
     probs, keep = record_problems(rargs)
+    with open(OWN_TABLE) as f:
+        own_rows = [ln for ln in f if not ln.startswith("#")]
     with open(args.table) as f:
         rows = list(csv.DictReader(f))
     os.makedirs(args.out_dir, exist_ok=True)
@@ -65,10 +77,14 @@ def main():
                              args.iters, [0], [0, 1, 2, 4, 8], 24)
         kstr = [str(x) for x in key]
         ship = [r for r in rows if [r[f] for f in blaslt.FIELDS[:15]] == kstr]
-        assert len(ship) == 1, prod
-        seen = {macro_tile(ship[0]["solution"])}
-        print(f"[{prod}] shipped {ship[0]['solution'][:70]} algo {ship[0]['algo']} wgm {ship[0]['wgm']} "
-              f"{ship[0]['us']} us", flush=True)
+        assert len(ship) <= 1, prod
+        # the own kernel's row for this product (row-major M = hipBLASLt n, N = hipBLASLt m)
+        own_key = f"{n},{m},{k},{int(bool(key[14]))},"
+        own_hit = [ln for ln in own_rows if ln.startswith(own_key)]
+        seen = {macro_tile(ship[0]["solution"])} if ship and not own_hit else set()
+        if ship:
+            print(f"[{prod}] table {ship[0]['solution'][:70]} algo {ship[0]['algo']} wgm {ship[0]['wgm']} "
+                  f"{ship[0]['us']} us" + ("  (own kernel in the step)" if own_hit else ""), flush=True)
         n_out = 0
         for algo, sk, wg, us, name in res:
             mt = macro_tile(name)
@@ -77,9 +93,12 @@ def main():
             seen.add(mt)
             n_out += 1
             alt = [dict(r) for r in rows]
-            for r in alt:
-                if [r[f] for f in blaslt.FIELDS[:15]] == kstr:
-                    r.update(algo=algo, splitk=sk, wgm=wg, us=f"{us:.2f}", solution=name)
+            new = dict(zip(blaslt.FIELDS[:15], kstr))
+            new.update(algo=algo, splitk=sk, wgm=wg, us=f"{us:.2f}", torch_us="", solution=name)
+            alt = [r for r in alt if [r[f] for f in blaslt.FIELDS[:15]] != kstr] + [new]
+            if own_hit:
+                with open(os.path.join(args.out_dir, f"{prod}_{n_out}.own.csv"), "w") as f:
+                    f.writelines(ln for ln in own_rows if ln not in own_hit)
             path = os.path.join(args.out_dir, f"{prod}_{n_out}.csv")
             with open(path, "w", newline="") as f:
                 w = csv.DictWriter(f, fieldnames=blaslt.FIELDS)
