@@ -76,6 +76,9 @@ def build_parser():
                     help="DeepSpeed JSON for zero2/zero3 (default configs/deepspeed/<strategy>.json)")
     ap.add_argument("--fsdp-wrap", default="block", choices=["block", "root"],
                     help="FSDP unit layout: per transformer block, or the reference's single root FlatParameter")
+    ap.add_argument("--ddp-shard-optimizer", action="store_true",
+                    help="ddp: shard the AdamW state over the ranks (torch DDP + ZeroRedundancyOptimizer; reported "
+                         "as ddp_zero1): reduce-scatter + all-gather instead of all-reduce, same update")
     ap.add_argument("--fsdp-sharding", default=None, choices=["full_shard", "shard_grad_op"],
                     help="FSDP sharding_strategy (default: configs/fsdp/fsdp_config.yaml's full_shard); "
                          "shard_grad_op keeps the gathered parameters from forward to backward (no re-gather)")
@@ -226,7 +229,8 @@ def run_rank(args) -> int:
                                grad_accum=args.grad_accum, accum_semantics=args.accum_semantics, dtype=args.dtype,
                                bucket_mb=bucket_mb, seed=42, grad_reduce=args.grad_reduce,
                                grad_comm_dtype=args.grad_comm_dtype,
-                               fsdp_wrap=args.fsdp_wrap, fsdp_sharding=args.fsdp_sharding)
+                               fsdp_wrap=args.fsdp_wrap, fsdp_sharding=args.fsdp_sharding,
+                               ddp_shard_optimizer=args.ddp_shard_optimizer)
         engine, ecfg = _engine_for(h, model, device)
         ds = SyntheticDataset(mcfg.vocab_size, args.seq_len, 1000, 42)
         batches = make_batcher("device", ds, args.per_device_batch, eworld, engine.comm.rank, args.strategy, device)
@@ -304,6 +308,8 @@ def run_rank(args) -> int:
         label = args.strategy
         if args.strategy == "zero2" and ecfg.zero_stage == 1:
             label = "zero1"                  # window-reduced: ZeRO-1 communication
+        if args.strategy == "ddp" and ecfg.zero_stage == 1:
+            label = "ddp_zero1"              # DDP + sharded optimizer state
         if args.strategy == "fsdp" and ecfg.wrap == "root":
             label = "fsdp_root"
         if args.strategy == "fsdp" and not ecfg.reshard_after_forward:

@@ -68,6 +68,9 @@ def build_parser():
     p.add_argument("--results-dir", type=str, required=True)
     # MI355X extras
     p.add_argument("--accum-semantics", choices=["reference", "uniform"], default="reference")
+    p.add_argument("--ddp-shard-optimizer", action="store_true",
+                   help="ddp: shard the AdamW state over the ranks (torch DDP + ZeroRedundancyOptimizer): "
+                        "reduce-scatter + all-gather instead of all-reduce, same update")
     p.add_argument("--grad-reduce", choices=["micro", "window"], default="micro",
                    help="ZeRO-2 gradient reduce-scatter every micro-step (DeepSpeed) or once per "
                         "accumulation window")
@@ -128,6 +131,8 @@ def _engine_for(args, model, device):
                         compute_dtype=DTYPES[args.dtype], bucket_mb=args.bucket_mb, seed=args.seed,
                         grad_reduce=getattr(args, "grad_reduce", "micro"))
     cfg.extra["grad_comm_dtype"] = "fp32" if getattr(args, "grad_comm_dtype", None) == "fp32" else "compute"
+    if args.strategy == "ddp" and getattr(args, "ddp_shard_optimizer", False):
+        cfg.extra["shard_optimizer"] = True       # DDP + ZeroRedundancyOptimizer (parallel/replicated.py)
     return make_engine(model, cfg, device), cfg
 
 

@@ -37,6 +37,9 @@ STRATS = {
     # gathered for the forward stay until the backward, so the backward re-gathers nothing (288 GB holds them)
     "fsdp_sgo": ["--strategy", "fsdp", "--fsdp-sharding", "shard_grad_op"],
     "fsdp_bf16_sgo": ["--strategy", "fsdp", "--dtype", "bf16", "--fsdp-sharding", "shard_grad_op"],
+    # DDP + ZeroRedundancyOptimizer: config #2's update with the optimizer state sharded (reduce-scatter +
+    # all-gather, the all-reduce's wire bytes) -- the replicated full-model AdamW every micro-step goes
+    "ddp_bf16_zero1": ["--strategy", "ddp", "--dtype", "bf16", "--ddp-shard-optimizer"],
 }
 
 

@@ -65,15 +65,18 @@ def _cfg(strategy, accum, **kw):
                                     "stage3_param_persistence_threshold": 300,
                                     "stage3_max_live_parameters": kw.pop("max_live", 1e9),
                                     "stage3_max_reuse_distance": 1e9}}
+    shard_opt = kw.pop("shard_optimizer", False)
     c = engine_config(strategy, accum, kw.pop("semantics", "reference"), ds, kw.pop("fsdp", None),
                       bucket_mb=0.01, grad_reduce=kw.pop("grad_reduce", "micro"))
+    if shard_opt:
+        c.extra["shard_optimizer"] = True
     for k, v in kw.items():
         setattr(c, k, v)
     return c
 
 
 CASES = [
-    ("ddp", 1, {}), ("ddp", 2, {"semantics": "uniform"}), ("zero2", 4, {}), ("zero2", 4, {"grad_reduce": "window"}),
+    ("ddp", 1, {}), ("ddp", 1, {"shard_optimizer": True}), ("ddp", 2, {"semantics": "uniform"}), ("zero2", 4, {}), ("zero2", 4, {"grad_reduce": "window"}),
     ("zero3", 4, {}), ("zero3", 4, {"max_live": 0}), ("fsdp", 1, {}),
     ("fsdp", 1, {"fsdp": {"auto_wrap_policy": "size_based"}}),
     ("fsdp", 1, {"fsdp": {"sharding_strategy": "shard_grad_op"}}),

@@ -54,7 +54,10 @@ def _cfg(strategy, accum, semantics="reference", **kw):
                                     "stage3_max_live_parameters": kw.pop("max_live", 1e9),
                                     "stage3_max_reuse_distance": 1e9}}
     fc = kw.pop("fsdp", None)
+    shard_opt = kw.pop("shard_optimizer", False)
     c = engine_config(strategy, accum, semantics, ds, fc, bucket_mb=kw.pop("bucket_mb", 0.01))
+    if shard_opt:
+        c.extra["shard_optimizer"] = True
     c.lr = 1e-3 if strategy in ("ddp", "fsdp") and semantics == "reference" else c.lr
     for k, v in kw.items():
         setattr(c, k, v)
@@ -133,6 +136,7 @@ def _worker(rank, world, port, strategy, accum, kw, out_path, global_batch=4):
 
 @pytest.mark.parametrize("strategy,accum,kw", [
     ("ddp", 1, {}),
+    ("ddp", 1, {"shard_optimizer": True}),  # DDP + ZeroRedundancyOptimizer: same training, sharded state
     ("ddp", 2, {"semantics": "uniform"}),
     ("zero2", 2, {}),
     ("zero2", 2, {"zero_stage": 1}),       # --grad-reduce window: one reduce-scatter per window
@@ -156,7 +160,7 @@ def test_world2_matches_single_process(strategy, accum, kw):
 
 
 @pytest.mark.parametrize("strategy,accum,kw", [("zero2", 2, {}), ("zero2", 2, {"zero_stage": 1}),
-                                               ("zero3", 2, {}), ("ddp", 1, {}),
+                                               ("zero3", 2, {}), ("ddp", 1, {}), ("ddp", 1, {"shard_optimizer": True}),
                                                ("fsdp", 1, {})])
 def test_world4_matches_single_process(strategy, accum, kw):
     """Four ranks (uneven bucket chunks, padding on every rank, prefetch across 4 shards) reproduce
@@ -228,6 +232,7 @@ def _worker_lazy(rank, *args):
 
 @pytest.mark.parametrize("strategy,accum,kw", [
     ("ddp", 1, {}),
+    ("ddp", 1, {"shard_optimizer": True}),  # DDP + ZeroRedundancyOptimizer: same training, sharded state
     ("ddp", 2, {"semantics": "uniform"}),
     ("zero2", 2, {}),
     ("zero2", 2, {"zero_stage": 1}),
