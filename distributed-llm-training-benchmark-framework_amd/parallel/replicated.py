@@ -83,11 +83,12 @@ class ReplicatedEngine(Engine):
             # shares the first bucket with two blocks and the blocks' dW batches come out 2/4/4/4/2
             # (a 2-block batch costs 75 us per block against 58 for 4, profiles/wgrad_batch_size_r2.txt)
             solo_head = int(cfg.extra.get("solo_head_units", os.environ.get("DLTB_SOLO_HEAD", 1)))
-            if self._ddp_pipe_wanted():
+            if self._ddp_pipe_wanted() or cfg.extra.get("shard_optimizer"):
                 # DDP with the optimizer pipelined per bucket: the last bucket's all-reduce is the exposed
                 # tail, so blocks 0 and 1 get buckets of their own (1-block dW batches, +~0.1 ms) and the
                 # tail shrinks from a 4-block bucket to one block: emulated ddp_bf16 N = 8 10.09 -> 9.97 ms
-                # (profiles/emulated_ddp_pipeline_r5.txt)
+                # (profiles/emulated_ddp_pipeline_r5.txt).  DDP + sharded optimizer: the last bucket's
+                # reduce-scatter is the exposed tail the same way: 9.46 -> 9.36 ms (emulated_ddp_zero1_r5.txt)
                 solo_tail = 3
         # the first bucket(s) after the head: twice the size (fewer collectives early in the backward,
         # while compute hides them; the buckets at its end -- the first parameter all-gathers of the
