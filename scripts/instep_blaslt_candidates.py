@@ -39,6 +39,10 @@ PRODUCTS = {
     "out.dgrad": (1, 0, 1024, 2048, 1024, 0),
     "fc1.dgrad": (1, 0, 1024, 2048, 4096, 0),
     "qkv.dgrad": (1, 0, 1024, 2048, 3072, 0),
+    # the tied head: logits, data gradient (K = vocab, split-K), weight gradient
+    "head.fwd": (1, 0, 32000, 2048, 1024, 0),
+    "head.dgrad": (1, 0, 1024, 2048, 32000, 0),
+    "head.wgrad": (1, 1, 1024, 32000, 2048, 0),
 }
 OWN_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "gemm_rs",
                          "gemm_rs_gfx950.csv")
@@ -54,6 +58,7 @@ def main():
     ap.add_argument("--products", default="fc1.fwd,fc2.dgrad,qkv.fwd")
     ap.add_argument("--top", type=int, default=3)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--splitk", default="0", help="split-K factors swept (comma list)")
     ap.add_argument("--table", default=blaslt.DEFAULT_FILE)
     ap.add_argument("--out-dir", default="gpurun_out/blaslt_ab")
     args = ap.parse_args()
@@ -74,7 +79,7 @@ def main():
         key, (a, b, c, acc, bias) = hits[0]
         _, opA, opB, m, n, k, batch, lda, ldb, ldc, sa, sb, sc, beta1, _ = key
         res = C.blaslt_sweep(b, a, c, opA, opB, m, n, k, batch, lda, ldb, ldc, sa, sb, sc, bool(beta1), bias,
-                             args.iters, [0], [0, 1, 2, 4, 8], 24)
+                             args.iters, [int(x) for x in args.splitk.split(",")], [0, 1, 2, 4, 8, 16], 24)
         kstr = [str(x) for x in key]
         ship = [r for r in rows if [r[f] for f in blaslt.FIELDS[:15]] == kstr]
         assert len(ship) <= 1, prod
