@@ -141,6 +141,8 @@ def train(args):
     args.world_size, args.rank, args.local_rank = world, rank, local_rank
     auto_bucket = args.bucket_mb is None
     label = args.strategy_label or args.strategy
+    if not args.strategy_label and args.strategy == "ddp" and getattr(args, "ddp_shard_optimizer", False):
+        label = "ddp_zero1"          # DDP + sharded optimizer state: its own row in metrics.csv
     ds_cfg = None
     if args.strategy in ("zero2", "zero3"):
         ds_cfg = load_deepspeed_config(args.deepspeed_config or default_config_path(args.strategy))
