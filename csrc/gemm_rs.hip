@@ -50,6 +50,9 @@ struct RsArgs {
   // part[m-tile][n] = the column sums of the rounded C over the tile's rows (the dGELU epilogue: aux = GELU'(f))
   const bf16_t* aux;
   float* part;
+  // fp32-image kernels only: gout = GELU(C) of the rounded C (row stride ldc) -- the fc1 forward's activation
+  // written by the producing GEMM instead of a separate elementwise pass over f
+  bf16_t* gout;
 };
 
 DLTB_DEV f32x4 mfma16(rs_frag a, rs_frag b, f32x4 c) {
@@ -182,6 +185,12 @@ struct RsEpiF {
       o.x = pack_bf2(v[0], v[1]);
       o.y = pack_bf2(v[2], v[3]);
       *reinterpret_cast<uint2*>(dst) = o;
+      if (g.gout) {                                    // GELU of the stored (rounded) f, as gelu_fwd_kernel
+        uint2 go;
+        go.x = pack_bf2(gelu_fwd_f(lo_bf(o.x)), gelu_fwd_f(hi_bf(o.x)));
+        go.y = pack_bf2(gelu_fwd_f(lo_bf(o.y)), gelu_fwd_f(hi_bf(o.y)));
+        *reinterpret_cast<uint2*>(g.gout + off) = go;
+      }
       if (g.part) {                                    // sum the rounded values the next GEMM reads
         cs[0] += lo_bf(o.x); cs[1] += hi_bf(o.x); cs[2] += lo_bf(o.y); cs[3] += hi_bf(o.y);
       }
@@ -1394,8 +1403,15 @@ bool dltb_gemm_rs_aux_supported(int M, int N, int K, int cfg) {
   return nt % cpr == 0 && kRsCfgs[cfg].bm * cpr / nt <= 16;   // the aux values prefetched (RsEpiF::AUX_PF)
 }
 
+bool dltb_gemm_rs_gelu_supported(int M, int N, int K, int cfg) {
+  // the GELU-output epilogue: any fp32-image kernel (kind 3)
+  if (cfg < 0) cfg = dltb_gemm_rs_pick(M, N, K);
+  return dltb_gemm_rs_supported(M, N, K, cfg) && kRsCfgs[cfg].kind == 3;
+}
+
 int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, const void* aux, float* part) {
+                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, const void* aux, float* part,
+                 void* gout) {
   if (cfg < 0) cfg = dltb_gemm_rs_pick(M, N, K);
   if (!dltb_gemm_rs_supported(M, N, K, cfg)) return -1;
   RsArgs g{};
@@ -1413,7 +1429,9 @@ int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long l
   g.accumulate = accumulate;
   g.aux = (const bf16_t*)aux;
   g.part = part;
+  g.gout = (bf16_t*)gout;
   if ((aux || part) && !dltb_gemm_rs_aux_supported(M, N, K, cfg)) return -1;
+  if (gout && (accumulate || !dltb_gemm_rs_gelu_supported(M, N, K, cfg))) return -1;
   launch_rs_cfg(cfg, g, st);
   return cfg;
 }

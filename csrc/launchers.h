@@ -166,7 +166,9 @@ int dltb_gemm_rs_pick(int M, int N, int K);
 bool dltb_gemm_rs_supported(int M, int N, int K, int cfg);
 int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
                  int N, int K, int accumulate, int cfg, int gm, hipStream_t st, const void* aux = nullptr,
-                 float* part = nullptr);
+                 float* part = nullptr, void* gout = nullptr);
+// C = A B^T + bias and gout = GELU(C) (of the rounded C) from one launch (fp32-image kernels)
+bool dltb_gemm_rs_gelu_supported(int M, int N, int K, int cfg);
 int dltb_gemm_rs_bm(int cfg);
 // C = (A B^T) * aux (elementwise, rounded once) with per-m-tile fp32 column partials of C (the dGELU epilogue)
 bool dltb_gemm_rs_aux_supported(int M, int N, int K, int cfg);

@@ -144,13 +144,19 @@ class _BlockFn(torch.autograd.Function):
                 model.site_attn(i + 1), part=0)
         else:
             x1, h2, mean2, rstd2 = F_.norm_fwd(x, a, ln2w, ln2b, LN_EPS, False, y_out=lb and lb.h2)
-        f = F_.linear_fwd(h2, w1, b1)
-        # dGELU-epilogue path (own-GEMM table): keep GELU'(f) for the backward instead of f
-        dgelu = f.is_cuda and F_.dgelu_fused(f.shape[0], f.shape[1], w2.shape[0])
-        if dgelu:
-            g, f = F_.gelu_fwd_grad(f, out=lb and lb.g)
+        # fc1 + GELU in one own-GEMM launch when the table has a GELU-epilogue row (bias = 3)
+        fg = F_.linear_fwd_gelu(h2, w1, b1, g_out=lb and lb.g)
+        if fg is not None:
+            f, g = fg
+            dgelu = False
         else:
-            g = F_.gelu_fwd(f, out=lb and lb.g)
+            f = F_.linear_fwd(h2, w1, b1)
+            # dGELU-epilogue path (own-GEMM table): keep GELU'(f) for the backward instead of f
+            dgelu = f.is_cuda and F_.dgelu_fused(f.shape[0], f.shape[1], w2.shape[0])
+            if dgelu:
+                g, f = F_.gelu_fwd_grad(f, out=lb and lb.g)
+            else:
+                g = F_.gelu_fwd(f, out=lb and lb.g)
         m = F_.linear_fwd_splitk(g, w2, b2) if model.splitk_planes else None
         if m is None:
             m = F_.linear_fwd(g, w2, b2)    # Dropout(m) + x1 happens in the consumer's LayerNorm

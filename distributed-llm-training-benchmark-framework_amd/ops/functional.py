@@ -213,6 +213,31 @@ def gelu_fwd_grad(f, out=None, gp_out=None):
 _DGELU = 2
 
 
+_GELU_OUT = 3              # own-GEMM table rows with bias = 3: bias + GELU-output epilogue (fc1 forward)
+
+
+def linear_fwd_gelu(x2d, w, b, g_out=None):
+    """(f, GELU(f)) = (x W^T + b, its GELU) from ONE own-GEMM launch (the epilogue writes both; GELU of
+    the rounded f, bitwise gelu_fwd's), when the own-GEMM table has a bias = 3 row for the shape; else None."""
+    global own_gemm_calls
+    if not (x2d.is_cuda and b is not None and x2d.dtype == torch.bfloat16 and x2d.dim() == 2):
+        return None
+    M, K = x2d.shape
+    N = w.shape[0]
+    hit = rs_table().get((M, N, K, _GELU_OUT))
+    if hit is None or not (x2d.stride(1) == 1 and w.stride(1) == 1 and x2d.stride(0) % 8 == 0
+                           and w.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+                           and b.is_contiguous() and b.data_ptr() % 8 == 0):
+        return None
+    f = torch.empty(M, N, dtype=x2d.dtype, device=x2d.device)
+    g = g_out if g_out is not None else torch.empty_like(f)
+    if g.stride(0) != f.stride(0) or g.stride(1) != 1:
+        return None
+    own_gemm_calls += 1
+    ext().gemm_rs(x2d, w, f, b, False, hit[0], hit[1], gelu_out=g)
+    return f, g
+
+
 def dgelu_fused(M, N, K):
     """True when the fc2 data gradient (M tokens, N = the MLP width, K = the model width) runs with the dGELU
     epilogue: the forward then keeps GELU'(f) instead of f (models/tinygpt.py)."""

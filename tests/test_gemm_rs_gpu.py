@@ -82,6 +82,29 @@ def test_model_step_issues_own_gemm():
     assert 5.0 < float(loss.item()) < 15.0
 
 
+@pytest.mark.parametrize("cfg", [35, 62])
+def test_gelu_out_epilogue(cfg):
+    """gemm_rs(..., gelu_out=g): f = a b^T + bias (fp32 reference) and g = GELU(f) of the ROUNDED f, bitwise
+    what the separate gelu_fwd kernel writes -- the fc1 forward with its activation fused (table bias = 3)."""
+    C = ext()
+    M, N, K = 2048, 4096, 1024
+    assert C.gemm_rs_gelu_supported(M, N, K, cfg)
+    assert not C.gemm_rs_gelu_supported(M, N, K, 34)      # register-epilogue kernel: no GELU output
+    torch.manual_seed(cfg)
+    a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    b = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    bias = (torch.randn(N, device="cuda") * 0.1).to(torch.bfloat16)
+    g = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    f = C.gemm_rs(a, b, None, bias, False, cfg, 4, gelu_out=g)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t() + bias.float()
+    tol = ref.abs().max().item() * 2 ** -7 + 1e-2
+    assert (f.float() - ref).abs().max().item() <= tol
+    assert torch.equal(g, C.gelu_fwd(f, None))
+    ref_g = torch.nn.functional.gelu(f.float())
+    assert (g.float() - ref_g).abs().max().item() <= 2e-2 * ref_g.abs().max().item() + 1e-2
+
+
 @pytest.mark.parametrize("cfg", [62])
 def test_dgelu_epilogue(cfg):
     """gemm_rs_aux: out = (a b^T) * aux rounded once, part = per-128-row column sums of the rounded out --
@@ -110,3 +133,39 @@ def test_dgelu_epilogue(cfg):
     # the partials sum the ROUNDED outputs, per 128-row tile
     ref_part = out.float().view(M // 128, 128, N).sum(1)
     assert torch.allclose(part, ref_part, rtol=1e-4, atol=1e-3)
+
+
+def _one_layer_grads(monkeypatch, table):
+    from dltb.models import build_model, get_model_config
+    from dltb.parallel import engine_config, make_engine
+    if table is None:
+        monkeypatch.delenv("DLTB_OWN_GEMM_TABLE", raising=False)
+    else:
+        monkeypatch.setenv("DLTB_OWN_GEMM_TABLE", os.path.join(ROOT, "configs", "gemm_rs", table))
+    F._rs_table = None
+    try:
+        torch.manual_seed(0)
+        cfg = get_model_config("A", 2048)
+        cfg.n_layer = 1
+        model = build_model(cfg)
+        eng = make_engine(model, engine_config("zero2", 1, "reference"), "cuda:0")
+        idx = torch.randint(0, cfg.vocab_size, (1, 2048), generator=torch.Generator().manual_seed(1)).cuda()
+        c0 = F.own_gemm_calls
+        loss = eng(idx, idx)[1]
+        eng.backward(loss)
+        torch.cuda.synchronize()
+        return float(loss.item()), eng.flat_grad.float().clone(), F.own_gemm_calls - c0
+    finally:
+        F._rs_table = None
+
+
+@pytest.mark.parametrize("table", ["ab_gelu62.csv", "ab_gelu35.csv", "ab_dgelu62.csv"])
+def test_model_fused_gelu_tables_track_shipped(table, monkeypatch):
+    """The model with a fused-GELU table row (forward GELU output, or the backward dGELU epilogue) trains like
+    the shipped table: same loss to bf16 noise, gradients within bf16 rounding of the changed products."""
+    l0, g0, n0 = _one_layer_grads(monkeypatch, None)
+    l1, g1, n1 = _one_layer_grads(monkeypatch, table)
+    assert n1 == n0 + 1, (n0, n1)                      # the fused product ran on the own kernel
+    assert abs(l1 - l0) < 2e-3 * abs(l0), (l0, l1)
+    rel = (g1 - g0).norm().item() / g0.norm().item()
+    assert rel < 2e-2, rel
