@@ -82,14 +82,13 @@ def test_model_step_issues_own_gemm():
     assert 5.0 < float(loss.item()) < 15.0
 
 
-@pytest.mark.parametrize("cfg", [35, 62])
+@pytest.mark.parametrize("cfg", [34, 35, 62])
 def test_gelu_out_epilogue(cfg):
     """gemm_rs(..., gelu_out=g): f = a b^T + bias (fp32 reference) and g = GELU(f) of the ROUNDED f, bitwise
     what the separate gelu_fwd kernel writes -- the fc1 forward with its activation fused (table bias = 3)."""
     C = ext()
     M, N, K = 2048, 4096, 1024
-    assert C.gemm_rs_gelu_supported(M, N, K, cfg)
-    assert not C.gemm_rs_gelu_supported(M, N, K, 34)      # register-epilogue kernel: no GELU output
+    assert C.gemm_rs_gelu_supported(M, N, K, cfg)      # fp32-image epilogue kernels (gemm_rsf)
     torch.manual_seed(cfg)
     a = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     b = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
