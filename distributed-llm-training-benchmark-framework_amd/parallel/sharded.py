@@ -238,6 +238,13 @@ class ShardedEngine(Engine):
                 off += g.total
         self.defer_wgrad = batch and (self.world == 1 or self._arena is not None)
         self._wq = WgradQueue()
+        # world 1: nothing reads a bias / norm-weight gradient before the end of the backward (the
+        # persistent slots are handed over in _finish_backward), so every block's column sums go to one
+        # shared reducer flushed there -- one or two colreduce launches instead of one per block, and the
+        # QKV-bias partials ride along with the next colpart launch, as in the replicated engines
+        from ..ops import functional as F_
+        self._red = F_.GradReducer(64, defer_plain=True) if (
+            dev.type == "cuda" and self.world == 1 and os.environ.get("DLTB_SHARED_RED", "1") == "1") else None
         self._pend = []              # completed groups whose dW / reduce-scatter wait for a batch
         self.wgrad_rows_reversed = self._blocks_reversed() if self.world == 1 else False
         # world 1: every group's gathered view IS its resident shard, so W^T can be cached per
@@ -469,6 +476,9 @@ class ShardedEngine(Engine):
         else:
             super().wgrad(unit, i, dy, x, dw, accumulate)
 
+    def grad_reducer(self):
+        return self._red
+
     def grads_ready(self, unit):
         self._reported.add(id(unit))
         if self._carry is not None and self._carry[0][0] is unit:
@@ -601,6 +611,8 @@ class ShardedEngine(Engine):
         # ws == 1: the group gradient buffers ARE the owner gradients; accumulate in place
 
     def _finish_backward(self):
+        if self._red is not None:
+            self._red.flush()
         self._wq.flush()
         self._flush_pending()                     # (their dW products were just issued)
         self._zero_unreported()                   # slots of units that never reported: zero

@@ -118,3 +118,34 @@ def test_splitk_planes_step_matches_hipblaslt_step():
     assert abs(res[0][0] - res[1][0]) < 1e-2 * abs(res[0][0]), (res[0][0], res[1][0])
     assert bool(torch.isfinite(res[1][1]).all())
     assert rel(res[1][1], res[0][1]) < 3e-2, rel(res[1][1], res[0][1])
+
+
+@pytest.mark.parametrize("strategy", ["zero3", "fsdp"])
+def test_sharded_world1_shared_column_reducer(strategy, monkeypatch):
+    """ZeRO-3 / FSDP at world 1 send every block's bias / norm-weight column sums to one shared reducer
+    flushed at the end of the backward (DLTB_SHARED_RED, parallel/sharded.py); training must match the
+    per-block reductions (same partial sums, fp32 adds in another grouping)."""
+    out = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("DLTB_SHARED_RED", on)
+        torch.manual_seed(0)
+        cfg = _cfg(T=512, layers=2)
+        eng = make_engine(build_model(cfg), engine_config(strategy, 2, "reference"), "cuda:0")
+        assert (eng._red is not None) == (on == "1")
+        eng.train()
+        g = torch.Generator().manual_seed(3)
+        losses = []
+        for _ in range(4):
+            idx = torch.randint(0, cfg.vocab_size, (1, 512), generator=g).cuda()
+            loss = eng(idx, idx)[1]
+            eng.backward(loss)
+            eng.step()
+            losses.append(float(loss.item()))
+        eng.finalize()
+        out.append((losses, eng.full_state_dict()))
+    (l0, s0), (l1, s1) = out
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 1e-3 * abs(a), (l0, l1)
+    for n in s0:
+        d = (s0[n].float() - s1[n].float()).abs().max().item()
+        assert d <= 1e-3 + 1e-2 * s0[n].float().abs().max().item(), (n, d)
