@@ -116,15 +116,23 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-# shipped emulated-fabric predictions (scripts/emulated_scaling.py), newest first: a real N-GPU run reports
-# the prediction for its own (strategy label, dtype, N) so the prediction error reads off one JSON line
-PREDICTION_TABLES = ["profiles/emulated_scaling_r5.jsonl", "profiles/emulated_scaling_r4_final.jsonl",
-                     "profiles/emulated_scaling_r4.jsonl"]
+# shipped emulated-fabric predictions (scripts/emulated_scaling.py): a real N-GPU run reports the prediction
+# for its own (strategy label, dtype, N) so the prediction error reads off one JSON line.  Tables are searched
+# newest first: by round, then a round's "_final" table before its earlier ones, then the letter suffix.
+def prediction_tables():
+    import glob
+    import re
+
+    def key(path):
+        m = re.match(r"emulated_scaling_r(\d+)([a-z]*)(_final)?", os.path.basename(path))
+        return (int(m.group(1)), bool(m.group(3)), m.group(2)) if m else (-1, False, "")
+    paths = glob.glob(os.path.join(ROOT, "profiles", "emulated_scaling_r*.jsonl"))
+    return [os.path.relpath(p, ROOT) for p in sorted(paths, key=key, reverse=True)]
 
 
 def predicted_row(parallelism: str, dtype: str, world: int):
     """The shipped prediction for this configuration, or None: {ms_per_step, value, table}."""
-    for rel in PREDICTION_TABLES:
+    for rel in prediction_tables():
         path = os.path.join(ROOT, rel)
         if not os.path.exists(path):
             continue
@@ -191,6 +199,7 @@ def run_rank(args) -> int:
     from dltb.comm.topology import recommend_bucket_mb
     from dltb.utils.dist import all_reduce_max, barrier, cleanup_distributed, setup_distributed
     from dltb.utils.timers import PhaseTimers
+    from dltb.ops import functional as F_
 
     resolve_precision(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -340,7 +349,8 @@ def run_rank(args) -> int:
                            "seq_len": args.seq_len,
                            "parallelism": f"{label}-dp{world}",
                            "grad_reduce": ecfg.extra.get("grad_reduce"),
-                           "grad_comm_dtype": args.grad_comm_dtype if args.strategy == "ddp" else None,
+                           "grad_comm_dtype": getattr(engine, "grad_comm_dtype", args.grad_comm_dtype)
+                           if args.strategy == "ddp" else None,
                            "bucket_mb": bucket_mb},
                 "strategy": args.strategy,
                 "world_size_seen": engine.comm.world,
@@ -365,6 +375,7 @@ def run_rank(args) -> int:
                 "same_strategy_precision_matches": (args.dtype == ref_dtype) if same else None,
                 "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
                 "gemm_tuning": tmode,
+                "torch_gemm_fallbacks": dict(F_.torch_fallbacks) or None,
                 "hip_graphs": graphed,
                 "ds_config_keys_ignored": sorted((ecfg.extra.get("ds_keys") or {}).get("ignored", {})),
                 "fabric_calibration": ({"fits": fabric["fits"], "rows": fabric["rows"],

@@ -102,6 +102,21 @@ def generate_report(csv_path: str, output_dir: str, platform: str = PLATFORM) ->
             v1 = "" if pd.isna(r["efficiency_vs_ws1_pct"]) else f"{r['efficiency_vs_ws1_pct']:.1f}"
             lines.append(f"| {str(r['strategy']).upper():8s} | {int(r['world_size']):9d} | "
                          f"{r['tokens_per_sec_per_gpu']:14,.0f} | {v1:>15s} | {r['efficiency_vs_min_ws_pct']:17.1f} |\n")
+        if "tokens_per_gpu_hour" in ext.columns:
+            priced = "tokens_per_sec_per_usd_hr" in ext.columns
+            lines += ["\n## Cost View\n\n",
+                      "Tokens one GPU processes per hour"
+                      + (f", and the reference's tokens/sec per $/hr at ${float(ext['gpu_hour_usd'].iloc[0]):.2f} "
+                         "per GPU-hour (tps / (world size x price))" if priced else
+                         " (set `--gpu-hour-usd` or `DLTB_GPU_HOUR_USD` for the $ columns)") + ".\n\n",
+                      "| Strategy | World Size | Seq Len | Tokens/GPU-hour |" + (" Tokens/sec per $/hr | Tokens/$ |" if priced else "") + "\n",
+                      "|----------|-----------|---------|-----------------|" + ("---------------------|----------|" if priced else "") + "\n"]
+            for _, r in ext.iterrows():
+                row = (f"| {str(r['strategy']).upper():8s} | {int(r['world_size']):9d} | {int(r['seq_len']):7d} | "
+                       f"{r['tokens_per_gpu_hour']:15,.0f} |")
+                if priced:
+                    row += f" {r['tokens_per_sec_per_usd_hr']:19,.0f} | {r['tokens_per_usd']:8,.0f} |"
+                lines.append(row + "\n")
     lines += ["\n---\n\n", "## Strategy Trade-offs\n\n"]
     titles = {"DDP": "DDP (Distributed Data Parallel)", "FSDP": "FSDP (Fully Sharded Data Parallel)",
               "ZERO2": "ZeRO-2", "ZERO3": "ZeRO-3"}

@@ -10,16 +10,20 @@ Output contract:
 * ``scaling_efficiency_pct`` uses the reference formula per (strategy, seq_len) group with more than
   one row: ``tps / (tps_of_first_row_at_min_ws * ws) * 100`` (single-row groups keep 100.0).  When
   the smallest world size in a group is 2 this reads 50 % for the 2-GPU row — reproduced verbatim
-  for CSV compatibility.  One deliberate deviation: the group key also holds the tier when a result
-  set mixes tiers at one (strategy, seq_len) -- the reference's long-sequence Tier B rows
-  (run_all_benchmarks.sh:49-51) would otherwise be the 1-GPU base of the Tier A rows (a 1-GPU Tier A
-  row read 487 % against the Tier B row of the same strategy and sequence length).
+  for CSV compatibility, including the grouping: a result set that mixes tiers at one (strategy,
+  seq_len) takes the first row at the smallest world size as the base, as the reference does.
 
-The corrected numbers go to ``metrics_extended.csv``: efficiency normalised to the group's WS=1 row
-(true weak-scaling efficiency), efficiency normalised to the smallest world size
-(``tps / (tps_min * ws / ws_min)``), per-GPU tokens/s, and the harness' extended sidecar fields when a
-``result.extended.json`` / ``result_*.extended.json`` sits next to the record.
+The corrected numbers go to ``metrics_extended.csv``: the reference formula grouped by tier too
+(``efficiency_tier_aware_pct``: the reference's long-sequence Tier B rows, run_all_benchmarks.sh:49-51,
+are otherwise the 1-GPU base of the Tier A rows -- a 1-GPU Tier A row reads 487 % against the Tier B
+row of the same strategy and sequence length), efficiency normalised to the group's WS=1 row (true
+weak-scaling efficiency), efficiency normalised to the smallest world size
+(``tps / (tps_min * ws / ws_min)``), per-GPU tokens/s, the cost view (tokens per GPU-hour; with a GPU
+price -- ``--gpu-hour-usd`` / ``DLTB_GPU_HOUR_USD`` -- the reference's "tokens/sec per $/hr" =
+tps / (ws x price), README.md:266-277 of the reference), and the harness' extended sidecar fields when
+a ``result.extended.json`` / ``result_*.extended.json`` sits next to the record.
 """
+import os
 import argparse
 import json
 from pathlib import Path
@@ -44,9 +48,11 @@ def load_records(results_dir):
     return records, sources
 
 
-def reference_efficiency(df: pd.DataFrame) -> pd.Series:
+def reference_efficiency(df: pd.DataFrame, by_tier: bool = False) -> pd.Series:
+    """The reference formula (scripts/parse_metrics.py:51-63): groups by (strategy, seq_len); ``by_tier``
+    adds the tier to the key (the extended CSV's corrected column)."""
     eff = pd.Series(100.0, index=df.index)
-    keys = ["strategy", "seq_len"] + (["tier"] if "tier" in df.columns else [])
+    keys = ["strategy", "seq_len"] + (["tier"] if by_tier and "tier" in df.columns else [])
     for _, grp in df.groupby(keys, sort=False):
         if len(grp) < 2:
             continue
@@ -57,10 +63,29 @@ def reference_efficiency(df: pd.DataFrame) -> pd.Series:
     return eff
 
 
-def extended_frame(df: pd.DataFrame, sources) -> pd.DataFrame:
+def gpu_hour_price(price=None):
+    """$ per GPU-hour for the cost view: the argument, else DLTB_GPU_HOUR_USD, else None (no $ column)."""
+    if price is None:
+        price = os.environ.get("DLTB_GPU_HOUR_USD")
+    try:
+        price = float(price) if price not in (None, "") else None
+    except ValueError:
+        price = None
+    return price if price and price > 0 else None
+
+
+def extended_frame(df: pd.DataFrame, sources, gpu_hour_usd=None) -> pd.DataFrame:
     ext = df[["strategy", "world_size", "seq_len", "tier", "tokens_per_sec", "mean_step_time_sec",
               "peak_vram_gb"]].copy()
     ext["tokens_per_sec_per_gpu"] = ext["tokens_per_sec"] / ext["world_size"]
+    ext["efficiency_tier_aware_pct"] = reference_efficiency(df, by_tier=True)
+    # cost view: tokens one GPU processes per hour; with a price, the reference's tokens/sec per $/hr
+    ext["tokens_per_gpu_hour"] = ext["tokens_per_sec_per_gpu"] * 3600.0
+    price = gpu_hour_price(gpu_hour_usd)
+    if price is not None:
+        ext["gpu_hour_usd"] = price
+        ext["tokens_per_sec_per_usd_hr"] = ext["tokens_per_sec"] / (ext["world_size"] * price)
+        ext["tokens_per_usd"] = ext["tokens_per_gpu_hour"] / price
     ext["efficiency_vs_ws1_pct"] = float("nan")
     ext["efficiency_vs_min_ws_pct"] = float("nan")
     for (_, _, _), grp in ext.groupby(["strategy", "seq_len", "tier"], sort=False):
@@ -92,7 +117,7 @@ def extended_frame(df: pd.DataFrame, sources) -> pd.DataFrame:
     return ext
 
 
-def parse_results(results_dir: str, output_dir: str):
+def parse_results(results_dir: str, output_dir: str, gpu_hour_usd=None):
     out = Path(output_dir)
     out.mkdir(parents=True, exist_ok=True)
     records, sources = load_records(results_dir)
@@ -109,7 +134,7 @@ def parse_results(results_dir: str, output_dir: str):
     csv = out / "metrics.csv"
     df.to_csv(csv, index=False)
     print(f"\nMetrics saved to: {csv}")
-    ext = extended_frame(df, srcs)
+    ext = extended_frame(df, srcs, gpu_hour_usd)
     ext.to_csv(out / "metrics_extended.csv", index=False)
     print("\n=== Summary ===")
     print(df[SUMMARY_COLS].to_string(index=False))
@@ -120,8 +145,10 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description="Parse benchmark results to CSV")
     ap.add_argument("--results-dir", required=True, help="Directory containing result JSON files")
     ap.add_argument("--out", required=True, help="Output directory for metrics.csv")
+    ap.add_argument("--gpu-hour-usd", type=float, default=None,
+                    help="$ per GPU-hour for the cost columns of metrics_extended.csv (default: $DLTB_GPU_HOUR_USD)")
     a = ap.parse_args(argv)
-    parse_results(a.results_dir, a.out)
+    parse_results(a.results_dir, a.out, a.gpu_hour_usd)
 
 
 if __name__ == "__main__":

@@ -29,6 +29,7 @@ from .models import build_model, get_model_config
 from .parallel.checkpoint import export_consolidated, load_checkpoint, save_checkpoint
 from .parallel.graphs import GraphedStep, graphs_enabled
 from .ops._ext import available as ext_available, so_path
+from .ops.functional import torch_fallbacks
 from .comm import describe as comm_describe
 from .parallel import STRATEGIES, engine_config, make_engine
 from .parallel.ds_config import ds_precision
@@ -330,8 +331,9 @@ def train(args):
             "memory": engine.memory_report(),
             "peak_vram_reserved_gb": (torch.cuda.max_memory_reserved(device) / 1e9) if device.type == "cuda" else 0.0,
             "accum_semantics": args.accum_semantics, "grad_reduce": args.grad_reduce, "dtype": args.dtype,
-            "grad_comm_dtype": args.grad_comm_dtype, "strategy_engine": args.strategy, "bucket_mb": args.bucket_mb, "data_loader": args.data_loader,
+            "grad_comm_dtype": getattr(engine, "grad_comm_dtype", args.grad_comm_dtype), "strategy_engine": args.strategy, "bucket_mb": args.bucket_mb, "data_loader": args.data_loader,
             "kernels": so_path(), "platform": device_info(device), "gemm_tuning": gemm_mode,
+            "torch_gemm_fallbacks": dict(torch_fallbacks) or None,
             "phase_times_ms": timers.summary() if timers is not None else None,
             "loss_scaler": engine.scaler.stats() if engine.scaler is not None else None,
             "deepspeed_config_keys": ecfg.extra.get("ds_keys") or None,

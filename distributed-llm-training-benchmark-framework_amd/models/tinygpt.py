@@ -152,7 +152,7 @@ class _BlockFn(torch.autograd.Function):
         else:
             f = F_.linear_fwd(h2, w1, b1)
             # dGELU-epilogue path (own-GEMM table): keep GELU'(f) for the backward instead of f
-            dgelu = f.is_cuda and F_.dgelu_fused(f.shape[0], f.shape[1], w2.shape[0])
+            dgelu = f.is_cuda and F_.dgelu_fused(f.shape[0], f.shape[1], w2.shape[0], f.dtype)
             if dgelu:
                 g, f = F_.gelu_fwd_grad(f, out=lb and lb.g)
             else:
@@ -202,8 +202,7 @@ class _BlockFn(torch.autograd.Function):
         w2t = rt.weight_t(unit, 10, w2)
         df = None
         if ctx.dgelu:                   # f holds GELU'(f): dGELU and the fc1 bias partials in the GEMM epilogue
-            df = F_.linear_dgrad_dgelu(dm, w2t, f, s[9][0], s[9][1], red, out=lb and lb.df)
-            assert df is not None, "dGELU epilogue planned in the forward but unavailable in the backward"
+            df = F_.dgelu_backward(dm, w2, w2t, f, s[9][0], s[9][1], red, out=lb and lb.df)
         else:
             dg = F_.linear_dgrad(dm, w2, w2t)
             df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)

@@ -216,46 +216,79 @@ _DGELU = 2
 _GELU_OUT = 3              # own-GEMM table rows with bias = 3: bias + GELU-output epilogue (fc1 forward)
 
 
+def _nt_operands_ok(*ts):
+    """Row-major 2-D bf16 operands with 16-byte aligned base and row stride (the own GEMM's 16-byte loads)."""
+    return all(t.dim() == 2 and t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+               and t.data_ptr() % 16 == 0 for t in ts)
+
+
 def linear_fwd_gelu(x2d, w, b, g_out=None):
     """(f, GELU(f)) = (x W^T + b, its GELU) from ONE own-GEMM launch (the epilogue writes both; GELU of
-    the rounded f, bitwise gelu_fwd's), when the own-GEMM table has a bias = 3 row for the shape; else None."""
+    the rounded f, bitwise gelu_fwd's), when the own-GEMM table has a bias = 3 row for the shape whose tile
+    config supports the GELU-output epilogue; else None (the caller runs GEMM + gelu_fwd)."""
     global own_gemm_calls
-    if not (x2d.is_cuda and b is not None and x2d.dtype == torch.bfloat16 and x2d.dim() == 2):
+    if not (x2d.is_cuda and b is not None and _nt_operands_ok(x2d, w)):
         return None
     M, K = x2d.shape
     N = w.shape[0]
     hit = rs_table().get((M, N, K, _GELU_OUT))
-    if hit is None or not (x2d.stride(1) == 1 and w.stride(1) == 1 and x2d.stride(0) % 8 == 0
-                           and w.stride(0) % 8 == 0 and x2d.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
-                           and b.is_contiguous() and b.data_ptr() % 8 == 0):
+    if hit is None or not (b.dtype == torch.bfloat16 and b.is_contiguous() and b.data_ptr() % 8 == 0
+                           and ext().gemm_rs_gelu_supported(M, N, K, hit[0])):
         return None
     f = torch.empty(M, N, dtype=x2d.dtype, device=x2d.device)
     g = g_out if g_out is not None else torch.empty_like(f)
-    if g.stride(0) != f.stride(0) or g.stride(1) != 1:
+    if g.stride(0) != f.stride(0) or g.stride(1) != 1 or g.data_ptr() % 16:
         return None
     own_gemm_calls += 1
     ext().gemm_rs(x2d, w, f, b, False, hit[0], hit[1], gelu_out=g)
     return f, g
 
 
-def dgelu_fused(M, N, K):
+def dgelu_fused(M, N, K, dtype=torch.bfloat16):
     """True when the fc2 data gradient (M tokens, N = the MLP width, K = the model width) runs with the dGELU
-    epilogue: the forward then keeps GELU'(f) instead of f (models/tinygpt.py)."""
-    return (M, N, K, _DGELU) in rs_table()
+    epilogue: the forward then keeps GELU'(f) instead of f (models/tinygpt.py).  Requires a bf16 step (the
+    GELU'-writing forward kernel is bf16-only) and a table row whose tile config supports the aux epilogue;
+    the backward still falls back (:func:`dgelu_backward`) when the engine has no cached W^T."""
+    hit = rs_table().get((M, N, K, _DGELU))
+    return hit is not None and dtype == torch.bfloat16 and ext().gemm_rs_aux_supported(M, N, K, hit[0])
 
 
 def linear_dgrad_dgelu(dy2d, wt, gp, db, accumulate, red, out=None):
     """df = (dY W) * GELU'(f) with the fc1 bias gradient's column partials, one own-GEMM launch
     (C = dY (W^T)^T; the epilogue multiplies by gp = GELU'(f) from the forward, rounds once and sums the rounded
-    columns per 128-row tile; the partials are reduced at ``red.flush()``).  None when the table has no row."""
+    columns per 128-row tile; the partials are reduced at ``red.flush()``).  None when the table has no row or
+    an operand's layout does not fit the kernel (the caller then takes :func:`dgelu_backward`'s fallback)."""
     global own_gemm_calls
+    if wt is None or red is None:
+        return None
     M, K = dy2d.shape
-    hit = rs_table().get((M, wt.shape[0], K, _DGELU))
-    if hit is None or red is None:
+    N = wt.shape[0]
+    hit = rs_table().get((M, N, K, _DGELU))
+    if hit is None or not _nt_operands_ok(dy2d, wt, gp) or not ext().gemm_rs_aux_supported(M, N, K, hit[0]):
+        return None
+    if out is not None and not (_nt_operands_ok(out) and out.stride(0) == gp.stride(0)):
         return None
     own_gemm_calls += 1
     df, part = ext().gemm_rs_aux(dy2d, wt, out, gp, hit[0], hit[1])
     red.add(part, db, accumulate)
+    return df
+
+
+def dgelu_backward(dm, w2, w2t, gp, db, accumulate, red, out=None):
+    """df = (dm W2) * GELU'(f) when the forward saved gp = GELU'(f): the fused own-GEMM epilogue, or -- when
+    that cannot run (no cached W^T on this engine, an operand layout the kernel refuses) -- the plain data
+    gradient, the product with gp in fp32 rounded once, and the fc1 bias column sum of the rounded df."""
+    df = linear_dgrad_dgelu(dm, w2t, gp, db, accumulate, red, out=out)
+    if df is not None:
+        return df
+    dg = linear_dgrad(dm, w2, w2t)
+    res = (dg.float() * gp.float()).to(dg.dtype)
+    df = _into(out, res)
+    if red is not None and df.is_cuda:
+        parts = ext().colpart([_PLAIN], [df], [None], [None], [None], [None], 0.0, None, [0])
+        red.add(parts[0][0], db, accumulate)
+    else:
+        colsum_into(df, db, accumulate)
     return df
 
 
@@ -379,7 +412,21 @@ def head_dgrad(dl, w, wt, g):
         C = ext()
         if C.gemm_supported(M, N, K, False, 2):
             return C.gemm(dl, wt, None, None, False, False, 4, 2, 0, 1, g)
+    if _gpu(dl):
+        _note_torch_fallback("head_dgrad", dl.shape, w.shape)
     return (torch.mm(dl, w) * g).to(dl.dtype)
+
+
+torch_fallbacks = {}        # op -> calls that ran a torch GEMM on the GPU (reported by bench.py / the harness)
+
+
+def _note_torch_fallback(op, *shapes):
+    """A GPU product that neither hipBLASLt's table nor an own kernel took: counted, and warned about once per op."""
+    n = torch_fallbacks.get(op, 0)
+    torch_fallbacks[op] = n + 1
+    if n == 0:
+        import warnings
+        warnings.warn(f"dltb: {op} {shapes} runs as a plain torch GEMM on the GPU (no tuned or own kernel)")
 
 
 # ------------------------------------------------------------------------------ attention

@@ -46,6 +46,20 @@ from .wgrad import WgradQueue
 _SPARSE_DEFER = os.environ.get("DLTB_SPARSE_DEFER", "1") == "1"
 
 
+def _dtype_name(dt):
+    return {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}.get(dt, str(dt))
+
+
+def grad_comm_dtype(stage: int, world: int, want_f32: bool, dt) -> str:
+    """The dtype the replicated engines' gradient collectives carry.  DDP (stage 0) widens each bucket to
+    fp32 on request (the reference's torch DDP reduces fp32 gradients); the sharded-optimizer DDP and
+    ZeRO-1/2 reduce-scatter the flat compute-dtype buffer, so an fp32 request is overridden there (half the
+    wire bytes of the fp32 all-reduce row; fp16 sums stay loss-scaled) and this is what results report."""
+    if want_f32 and stage == 0:
+        return "fp32"
+    return _dtype_name(dt)
+
+
 class ReplicatedEngine(Engine):
     name = "ddp"
     grad_write_ahead = True      # every gradient slot is a view of the flat buffer from the start
@@ -125,9 +139,15 @@ class ReplicatedEngine(Engine):
         # each bucket is widened into an fp32 buffer right before its all-reduce, summed over the
         # ranks in fp32, and AdamW reads the fp32 sum (2x the wire bytes, no bf16 rounding per hop)
         self.comm_f32 = None
-        if self.stage == 0 and self.world > 1 and cfg.extra.get("grad_comm_dtype") == "fp32" \
-                and dt != torch.float32:    # (fp16 grads are S-scaled: their fp32 sum cannot overflow)
+        want_f32 = cfg.extra.get("grad_comm_dtype") == "fp32"
+        self.grad_comm_dtype = grad_comm_dtype(self.stage, self.world, want_f32, dt)
+        if self.grad_comm_dtype == "fp32" and self.world > 1 and dt != torch.float32:
+            # (fp16 grads are S-scaled: their fp32 sum cannot overflow)
             self.comm_f32 = torch.zeros(L.total, dtype=torch.float32, device=dev)
+        elif want_f32 and self.world > 1 and dt != torch.float32:
+            import warnings
+            warnings.warn(f"grad_comm_dtype fp32 is not implemented for ZeRO stage {self.stage}: gradients are "
+                          f"reduced in {self.grad_comm_dtype}")
         for s in L.slots.values():
             p = s.unit.params[s.index]
             p.data = self.flat_param[s.offset:s.offset + s.numel].view(s.shape)

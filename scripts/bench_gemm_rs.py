@@ -23,7 +23,7 @@ from dltb.ops import blaslt  # noqa: E402
 from dltb.ops._ext import ext  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from bench_gemm_nt import graph_time, products  # noqa: E402
+from gemm_bench_util import graph_time, products  # noqa: E402
 
 
 def main():
@@ -38,7 +38,7 @@ def main():
     C = ext()
     blaslt.load()
     M, prods = products(a.model)
-    cfgs = [int(c) for c in a.cfgs.split(",") if c != ""] or list(range(16))
+    cfgs = [int(c) for c in a.cfgs.split(",") if c != ""] or list(range(15))
     gms = [int(g) for g in a.gm.split(",")]
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda") if a.cold else None
     tot_ref, tot_best = 0.0, 0.0

@@ -10,15 +10,9 @@ import torch  # noqa: E402
 import dltb  # noqa: E402,F401
 from dltb.ops._ext import ext  # noqa: E402
 
-TILE = {0: (128, 64), 1: (128, 64), 2: (128, 64), 3: (128, 256), 4: (128, 256), 5: (128, 192), 6: (128, 128),
-        7: (64, 128), 8: (128, 64), 9: (128, 64), 10: (128, 256), 11: (128, 192), 12: (128, 128),
-        13: (128, 64), 14: (128, 64), 15: (128, 64), 26: (128, 64), 27: (128, 64), 28: (128, 64),
-        29: (128, 256), 30: (128, 192), 31: (128, 128), 32: (128, 64), 33: (128, 64), 34: (128, 64),
-        35: (128, 256), 36: (128, 192), 37: (128, 128), 43: (128, 256), 49: (128, 64), 50: (128, 64), 51: (128, 64),
-        52: (128, 64), 53: (128, 64), 54: (128, 64), 55: (128, 256), 56: (128, 256), 57: (128, 192), 58: (128, 192),
-        59: (128, 256), 60: (128, 64), 61: (128, 192),
-        62: (128, 256), 63: (128, 256), 64: (128, 192), 65: (128, 64), 66: (128, 64),
-        67: (128, 256), 68: (128, 192), 69: (128, 64)}
+TILE = {0: (128, 64), 1: (128, 256), 2: (128, 192), 3: (128, 128), 4: (128, 64), 5: (128, 64), 6: (128, 256),
+        7: (128, 192), 8: (128, 64), 9: (128, 64), 10: (128, 64), 11: (128, 64), 12: (128, 64), 13: (128, 64),
+        14: (128, 64)}
 C = ext()
 REPS = int(os.environ.get("REPS", "10"))
 torch.manual_seed(0)
@@ -26,7 +20,7 @@ for (M, N, K) in [(2048, 3072, 1024), (4096, 1024, 1024), (2048, 1024, 4096), (2
     x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
     ref = x.float() @ w.float().t()
-    for c in [int(v) for v in os.environ.get("CFGS", "32,33,34,35,36,37").split(",")]:
+    for c in [int(v) for v in os.environ.get("CFGS", ",".join(str(c) for c in TILE)).split(",")]:
         if not C.gemm_rs_supported(M, N, K, c):
             continue
         bm, bn = TILE[c]

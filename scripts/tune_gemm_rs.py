@@ -2,7 +2,7 @@
 """Pick, per per-layer product of a model, the own MFMA GEMM config (csrc/gemm_rs.hip) that beats the tuned
 hipBLASLt solution, and write the own-GEMM table that ops/functional.py dispatches from.
 
-    python scripts/tune_gemm_rs.py [--model A|M7B] [--cfgs 26,27,...] [--min-gain 0.03]
+    python scripts/tune_gemm_rs.py [--model A|M7B] [--cfgs 0,9,...] [--min-gain 0.03]
                                    [--out configs/gemm_rs/gemm_rs_gfx950.csv]
 
 Per product (forward x W^T with the bias the model uses, data gradient dY (W^T)^T without): hipBLASLt (the
@@ -22,7 +22,7 @@ from dltb.ops import blaslt  # noqa: E402
 from dltb.ops._ext import ext  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from bench_gemm_nt import graph_time, products  # noqa: E402
+from gemm_bench_util import graph_time, products  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="A")
-    ap.add_argument("--cfgs", default="26,27,28,29,30,31")
+    ap.add_argument("--cfgs", default="0,4,5,9,10,11,12,13,14")
     ap.add_argument("--gm", default="1,4")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--min-gain", type=float, default=0.03)

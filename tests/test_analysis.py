@@ -128,3 +128,38 @@ def test_emulated_suite_labels_predictions(tmp_path):
     assert abs(z8["scaling_efficiency_pct"] - 100 * 7.0 / 8.5) < 0.01       # vs its measured WS=1 row
     res = json.loads((out / "bench-master-zero2_pred-ws8-seq2048_results" / "result.json").read_text())
     assert res["prediction"] is True and res["emulated_world"] == 8
+
+
+def test_cost_view_matches_reference_tokens_per_dollar(tmp_path):
+    """The reference's cost table (README.md:266-277): tokens/sec per $/hr = tps / (GPUs x $/GPU-hr), ZeRO-2 on
+    4 x A10 at $1.50 = 3,025.  metrics.csv keeps its 13 + 1 columns; the cost view lives in metrics_extended.csv
+    and the report."""
+    _write_published(tmp_path / "results")
+    parse_results(str(tmp_path / "results"), str(tmp_path / "summary"), gpu_hour_usd=1.5)
+    assert (tmp_path / "summary" / "metrics.csv").read_text().splitlines()[0] == CSV_HEADER
+    ext = pd.read_csv(tmp_path / "summary" / "metrics_extended.csv")
+    z2 = ext[(ext.strategy == "zero2") & (ext.world_size == 4)].iloc[0]
+    assert z2["tokens_per_sec_per_usd_hr"] == pytest.approx(18147 / (4 * 1.5))      # 3,024.5 -> "3,025"
+    assert z2["tokens_per_gpu_hour"] == pytest.approx(18147 / 4 * 3600)
+    assert z2["tokens_per_usd"] == pytest.approx(18147 / 4 * 3600 / 1.5)
+    rep = generate_report(str(tmp_path / "summary" / "metrics.csv"), str(tmp_path / "summary")).read_text()
+    assert "## Cost View" in rep and "3,02" in rep
+
+
+def test_mixed_tiers_keep_reference_grouping(tmp_path):
+    """ADVICE r5: metrics.csv groups by (strategy, seq_len) exactly as the reference does, even across tiers;
+    the tier-aware efficiency is a metrics_extended.csv column."""
+    rows = [("zero2", 1, "A", 280000.0), ("zero2", 2, "A", 500000.0), ("zero2", 1, "B", 60000.0)]
+    for s, ws, tier, tps in rows:
+        d = tmp_path / "r" / f"{s}-{ws}-{tier}_results"
+        d.mkdir(parents=True)
+        rec = dict(zip(RESULT_KEYS, (s, ws, 0, 2048, tier, 10, 1, 4, tps, 1.0, 5.0, 1.0, 1e-5)))
+        (d / "result.json").write_text(json.dumps(rec))
+    df = parse_results(str(tmp_path / "r"), str(tmp_path / "s"))
+    # reference: base = the first row at the smallest world size of the (strategy, seq_len) group
+    base = df[df.world_size == 1].iloc[0]["tokens_per_sec"]
+    a2 = df[(df.world_size == 2)].iloc[0]
+    assert a2["scaling_efficiency_pct"] == pytest.approx(500000.0 / (base * 2) * 100)
+    ext = pd.read_csv(tmp_path / "s" / "metrics_extended.csv", dtype={"tier": str})
+    e2 = ext[(ext.world_size == 2)].iloc[0]
+    assert e2["efficiency_tier_aware_pct"] == pytest.approx(500000.0 / (280000.0 * 2) * 100)

@@ -106,7 +106,7 @@ def test_own_gemm_table_parsing(tmp_path, monkeypatch):
     monkeypatch.delenv("DLTB_OWN_GEMM_TABLE")
     F._rs_table = None
     shipped = F.rs_table()
-    assert shipped and all(v[0] in (34, 49, 50) for v in shipped.values())
+    assert shipped and all(0 <= v[0] <= 14 for v in shipped.values())   # production configs (15+: ablations)
     F._rs_table = None
 
 
@@ -124,3 +124,26 @@ def test_table_paths_resolve_from_any_cwd(tmp_path, monkeypatch):
         resolve_config_path("configs/blaslt/no_such_table.csv", "t")
     with pytest.raises(FileNotFoundError):
         resolve_config_path(str(tmp_path / "missing.csv"), "t")
+
+
+def test_prediction_lookup_reads_the_newest_table():
+    """every shipped (parallelism, dtype, N) row resolves from the NEWEST prediction table, so
+    the first real multi-GPU run compares against the current prediction, not an older round's."""
+    sys.path.insert(0, ROOT)
+    import bench
+    tables = bench.prediction_tables()
+    assert tables, "no shipped prediction table"
+    newest = tables[0]
+    rows = [json.loads(ln) for ln in open(os.path.join(ROOT, newest)) if ln.strip()]
+    rows = [r for r in rows if r.get("prediction")]
+    assert rows
+    for r in rows:
+        got = bench.predicted_row(r["config"]["parallelism"], r["dtype"], r["emulated_world"])
+        assert got is not None and got["table"] == newest, (r["config"]["parallelism"], got)
+        assert got["ms_per_step"] == r["ms_per_step"]
+    # a round's "_final" table sorts before the same round's earlier one
+    names = [os.path.basename(t) for t in tables]
+    for i, n in enumerate(names):
+        if n.endswith("_final.jsonl"):
+            base = n.replace("_final", "")
+            assert base not in names[:i], (base, n)

@@ -255,3 +255,17 @@ def test_world2_lazy_collectives_match_single_process(strategy, accum, kw):
     ref = _train(strategy, _batches(STEPS, 4), 0, 1, accum, **dict(kw))
     for n in ref:
         assert _close(got[n], ref[n], n, 2e-5), (strategy, n, (got[n] - ref[n]).abs().max())
+
+
+
+def test_reported_grad_comm_dtype_is_the_one_reduced():
+    """the sharded-optimizer DDP (stage 1) reduce-scatters the compute-dtype buffer; an fp32 request
+    is overridden and the engine reports the dtype its collectives actually carry (bench.py / harness read it)."""
+    from dltb.parallel.replicated import grad_comm_dtype
+    assert grad_comm_dtype(0, 8, True, torch.float16) == "fp32"       # ddp fp16: fp32 all-reduce
+    assert grad_comm_dtype(0, 8, False, torch.bfloat16) == "bf16"
+    assert grad_comm_dtype(1, 8, True, torch.float16) == "fp16"       # ddp_zero1: not widened
+    assert grad_comm_dtype(1, 8, True, torch.bfloat16) == "bf16"
+    assert grad_comm_dtype(2, 8, True, torch.bfloat16) == "bf16"
+    eng = make_engine(_model(), _cfg("ddp", 1), "cpu")
+    assert eng.grad_comm_dtype == "fp32"                               # CPU engines compute in fp32
