@@ -130,8 +130,9 @@ def prediction_tables():
     return [os.path.relpath(p, ROOT) for p in sorted(paths, key=key, reverse=True)]
 
 
-def predicted_row(parallelism: str, dtype: str, world: int):
-    """The shipped prediction for this configuration, or None: {ms_per_step, value, table}."""
+def predicted_row(parallelism: str, dtype: str, world: int, seq_len: int = None, model: str = None):
+    """The shipped prediction for this configuration, or None: {ms_per_step, value, table, seq_len, model}.
+    ``seq_len`` / ``model`` (the JSON line's config fields), when given, must match the predicted run too."""
     for rel in prediction_tables():
         path = os.path.join(ROOT, rel)
         if not os.path.exists(path):
@@ -142,9 +143,13 @@ def predicted_row(parallelism: str, dtype: str, world: int):
                     d = json.loads(line)
                 except ValueError:
                     continue
+                c = d.get("config", {})
                 if (d.get("prediction") and d.get("emulated_world") == world and d.get("dtype") == dtype
-                        and d.get("config", {}).get("parallelism") == parallelism):
-                    return {"ms_per_step": d.get("ms_per_step"), "value": d.get("value"), "table": rel}
+                        and c.get("parallelism") == parallelism
+                        and (seq_len is None or c.get("seq_len") == seq_len)
+                        and (model is None or c.get("model") == model)):
+                    return {"ms_per_step": d.get("ms_per_step"), "value": d.get("value"), "table": rel,
+                            "seq_len": c.get("seq_len"), "model": c.get("model")}
     return None
 
 
@@ -386,7 +391,8 @@ def run_rank(args) -> int:
                 # a real multi-rank run explains itself: RCCL build and knobs, the in-job fabric fit
                 # (fabric_calibration), the measured phase split (phase_ms, eager ranks) and the
                 # shipped prediction for exactly this configuration
-                pred = predicted_row(f"{label}-dp{world}", out["dtype"], world)
+                pred = predicted_row(f"{label}-dp{world}", out["dtype"], world, out["config"]["seq_len"],
+                                     out["config"]["model"])
                 out["comm_env"] = comm_environment()
                 out["predicted"] = pred
                 out["prediction_error"] = ((ms - pred["ms_per_step"]) / pred["ms_per_step"]

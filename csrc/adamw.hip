@@ -132,16 +132,15 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
     const G* __restrict__ grad, const int* __restrict__ blk_seg, const int64_t* __restrict__ blk_start,
     const int64_t* __restrict__ seg_ostart, const int64_t* __restrict__ seg_len,
     const int64_t* __restrict__ seg_dst, const float* __restrict__ gscale, const float* __restrict__ hp,
-    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int wide_ab,
-    int nblk) {
+    float lr, float beta1, float beta2, float eps, float wd, float step_size, float inv_sqrt_bc2, int nblk) {
   if (hp) {   // step-dependent hyper-parameters from device memory (HIP-graph replays)
     if (hp[3] != 0.f) return;   // dynamic loss scaling found an inf / nan: the step is skipped
     lr = hp[0];
     step_size = hp[1];
     inv_sqrt_bc2 = hp[2];
   }
-  // one table row per block, or (a grid capped below the row count: DDP's early per-bucket updates
-  // trickling beside the backward on a side stream) a block-strided walk over the rows
+  // one table row per block, or (a grid capped below the row count: an update trickled beside other
+  // kernels) a block-strided walk over the rows
   for (int bi = blockIdx.x; bi < nblk; bi += gridDim.x) {
   const int seg = blk_seg[bi];
   const int64_t start = blk_start[bi];
@@ -152,16 +151,10 @@ __global__ __launch_bounds__(kAdamThreads) void adamw_kernel(
   const int64_t dst_base = start - s0;
   const AdamHp h{lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, gscale ? *gscale : 1.f};
   // every state element is touched once per step: streamed past the caches (nontemporal loads and
-  // stores).  The step's path is W = 4 (every fp32 access one coalesced 16-byte vector per lane, the
-  // 16-bit streams 8 bytes per lane): the W = 8 path (two adjacent float4 per lane, 32-byte lane stride
-  // per instruction) measured 4.22 TB/s against 5.52 for W = 4 on the TinyGPT-A state
-  // (profiles/adamw_r5.txt) and is kept only as the DLTB_ADAM_WIDE=1 A/B.  16-byte accesses need
-  // 8-element alignment of the owner offset, the segment length and the destination.
-  const bool wide = wide_ab && ((s0 | seg_len[seg]) & 7) == 0 && (((uintptr_t)dst) & 15) == 0;
-  if (wide) adamw_block<G, 8>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
-  else if (blockDim.x == kAdamThreads / 2)   // A/B (DLTB_ADAM_T128=1): half the lanes, twice the loads in flight each
-    adamw_block<G, 4, kAdamThreads / 2>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
-  else adamw_block<G, 4>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
+  // stores).  W = 4: every fp32 access one coalesced 16-byte vector per lane, the 16-bit streams 8 bytes
+  // per lane (a W = 8 path -- two adjacent float4 per lane -- measured 4.22 TB/s against 5.52 on the
+  // TinyGPT-A state, and 128-thread blocks no faster: profiles/adamw_r5.txt; both removed in round 6).
+  adamw_block<G, 4>(master, exp_avg, exp_avg_sq, grad, dst, start, seg_end, dst_base, h);
   }
 }
 
@@ -274,16 +267,15 @@ void dltb_adamw(float* master, float* exp_avg, float* exp_avg_sq, const void* gr
                 float inv_sqrt_bc2, int grid_cap, hipStream_t st) {
   if (nblocks <= 0) return;
   const int grid = grid_cap > 0 && grid_cap < nblocks ? grid_cap : nblocks;
-  static const int wide = getenv("DLTB_ADAM_WIDE") ? atoi(getenv("DLTB_ADAM_WIDE")) : 0;   // A/B: 16-byte path
-  static const int thr = getenv("DLTB_ADAM_T128") && atoi(getenv("DLTB_ADAM_T128")) ? kAdamThreads / 2 : kAdamThreads;
+  const int thr = kAdamThreads;
   if (grad_bf16)
     hipLaunchKernelGGL(adamw_kernel<bf16_t>, dim3(grid), dim3(thr), 0, st, master,
                        exp_avg, exp_avg_sq, (const bf16_t*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide, nblocks);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, nblocks);
   else
     hipLaunchKernelGGL(adamw_kernel<float>, dim3(grid), dim3(thr), 0, st, master,
                        exp_avg, exp_avg_sq, (const float*)grad, blk_seg, blk_start, seg_ostart,
-                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, wide, nblocks);
+                       seg_len, seg_dst, gscale, hp, lr, beta1, beta2, eps, wd, step_size, inv_sqrt_bc2, nblocks);
 }
 
 int dltb_sumsq_partials() { return kSumsqBlocks; }

@@ -38,14 +38,10 @@
 // pack it into v_pk_* ops, which beside MFMAs cost more issue time than the two scalar ops they
 // replace (docs/MI355X_HW_NOTES.md, packed f32 VALU beside MFMAs; measured 1-3 % slower,
 // profiles/attention_ab_r2.txt).
-// DLTB_ATTN_PIPE=1: the backward kernels compute S / dP of BOTH 32-row sub-tiles of a
-// 64-row tile before the first softmax, so one sub-tile's MFMAs run under the other's VALU softmax
-// inside the same wave.  Default 0 (sub-tile after sub-tile): measured equal or faster on MI355X
-// (TinyGPT-A dK/dV 56.2-57.2 vs 58.5-59.0 us, profiles/attention_ab_r2.txt).
-#ifndef DLTB_ATTN_PIPE
-#define DLTB_ATTN_PIPE 0
-#endif
-
+// The dK/dV kernel at D = 128 computes S / dP of both 32-row sub-tiles of a 64-row tile before the
+// first softmax, so one sub-tile's MFMAs run under the other's VALU softmax; at D = 64 sub-tile after
+// sub-tile measured equal or faster (TinyGPT-A dK/dV 56.2-57.2 vs 58.5-59.0 us, profiles/attention_ab_r2.txt;
+// the D = 64 both-sub-tile variants of dK/dV and dQ were removed in round 6).
 #ifndef DLTB_ATTN_LPT
 #define DLTB_ATTN_LPT 1   // causal fwd / dQ grids heaviest-first (profiles/attn_lpt_order_m7b_r3.txt)
 #endif
@@ -61,20 +57,6 @@
 #ifndef DLTB_DQ_KS64
 #define DLTB_DQ_KS64 3
 #endif
-// forward ping-pong at D = 64 (KS = 2): split 1 runs its tiles half an iteration behind split 0
-// (softmax + P V of the previous tile, then S of this one), so on every SIMD one wave's MFMAs run
-// beside the other's softmax inside the same barrier interval instead of both waves doing the same
-// phase at once.  A/B: csrc/build.py --tag pp -D DLTB_FWD_PP=1 -D DLTB_FWD_KS64=2
-#ifndef DLTB_FWD_PP
-#define DLTB_FWD_PP 0
-#endif
-#ifndef DLTB_FWD_PP_NST
-#define DLTB_FWD_PP_NST 3     // ring depth under the ping-pong (4: the lagging split refills 2 stages ahead)
-#endif
-#ifndef DLTB_FWD_PP_PRIO
-#define DLTB_FWD_PP_PRIO 0    // 1: s_setprio 1 on the lagging split, 2: on the leading split
-#endif
-
 #include "attn_mask.h"
 #include "common.h"
 #include "mfma_tiles.h"
@@ -294,7 +276,7 @@ template <int D, bool C = false>
 constexpr int fwd_ks() { return D == 64 ? (C && DLTB_CAUSAL_KS_CAP && DLTB_FWD_KS64 > 3 ? 3 : DLTB_FWD_KS64) : 2; }
 template <int D, int KS>
 constexpr int fwd_nst() {   // LDS ring depth (D = 128: 2 x 2 splits x 33 KiB)
-  return D == 64 && KS == 2 && DLTB_FWD_PP ? DLTB_FWD_PP_NST : (D == 64 && KS < 4 ? 3 : 2);
+  return D == 64 && KS < 4 ? 3 : 2;
 }
 template <int D>
 constexpr int fwd_stage_bytes() { return 2 * kTile * D * 2 + 1024; }   // K, V, dropout words of 4 waves
@@ -360,15 +342,9 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   for (int dt = 0; dt < NACC; ++dt)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) vfo[dt][hf] = tr_lane_off<D>(dt * 32, hf, lane);
-  constexpr bool PP = DLTB_FWD_PP && KS == 2 && NST >= 3;
   wait_vm<0>();        // Q fragments landed: no compiler vmcnt wait for them inside the loop
-  if (PP && spu == 1) {                          // (the lagging split refills NST - 2 stages ahead)
 #pragma unroll
-    for (int i = 0; i < NST - 2; ++i) issue(i);
-  } else {
-#pragma unroll
-    for (int i = 0; i < NST - 1; ++i) issue(i);
-  }
+  for (int i = 0; i < NST - 1; ++i) issue(i);
 
   f32x16 oacc[NACC];
 #pragma unroll
@@ -466,35 +442,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(AttnArgs P) {
   };
   auto visible = [&](int t) { return t < nt && (!CAUSAL || t * kTile <= q0 + 31); };
 
-  if (PP && spu == 1) {
-    // ---- lagging split: [softmax + P V of tile it-1] [S of tile it] per barrier interval.  Its
-    // refill runs one stage ahead (into the slot of tile it-2, done in the previous interval),
-    // so exactly one stage is in flight at each wait.
-    constexpr int AH = NST - 2;                  // stages issued ahead
-    static_assert(!PP || AH == 1 || AH == 2, "lagging ring depth");
-    if (DLTB_FWD_PP_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-    bool pend = false;
-    for (int it = 0; it < nit; ++it) {
-      const int t = it * KS + spu;
-      if (AH == 2 && it + 1 < nit && (it + 1) * KS + spu < nt) wait_vm<(AH == 2 ? GL : 0)>();
-      else wait_vm<0>();
-      __builtin_amdgcn_s_barrier();
-      issue(it + AH);
-      if (pend) {
-        const char* pst = stage_ptr(it - 1);
-        softmax();
-        pv(pst + TB, mask_word(pst));
-      }
-      pend = visible(t);
-      if (pend) s_tile(stage_ptr(it), t * kTile);
-    }
-    if (pend) {
-      const char* pst = stage_ptr(nit - 1);
-      softmax();
-      pv(pst + TB, mask_word(pst));
-    }
-  } else {
-    if (PP && DLTB_FWD_PP_PRIO == 2) __builtin_amdgcn_s_setprio(1);
+  {
     for (int it = 0; it < nit; ++it) {
       const int t = it * KS + spu;                   // wave-uniform: the tile branches are scalar
       // stages it+1 .. it+NST-2 (issued only if their tiles exist for this split) may stay in flight
@@ -807,7 +755,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
       }
     };
     if (t < nT) {
-      if ((D == 128 || DLTB_ATTN_PIPE) && (!CAUSAL || t * kTile >= k0 + 31)) {
+      if (D == 128 && (!CAUSAL || t * kTile >= k0 + 31)) {
         // full tile (no mask): both sub-tiles' S/dP first, so the second pair's MFMAs overlap the
         // first sub-tile's softmax, and its dV/dK MFMAs overlap the second softmax
         f32x16 sa0, dp0, sa1, dp1, pd, ds;
@@ -1056,15 +1004,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(AttnArgs P) {
       }
     };
     if (t < nt) {
-      if (DLTB_ATTN_PIPE && D == 64 && (!CAUSAL || kv0 + kTile - 1 <= q0)) {   // (D = 128: registers)
-        // full tile: both sub-tiles' S / dP first, so sub-tile 1's MFMAs run under sub-tile 0's
-        // softmax and sub-tile 0's dQ MFMAs under sub-tile 1's softmax
-        f32x16 sa0, dp0, sa1, dp1;
-        sdp(0, sa0, dp0);
-        sdp(1, sa1, dp1);
-        fin(0, sa0, dp0);
-        fin(1, sa1, dp1);
-      } else {
+      {
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
           if (CAUSAL && kv0 + 32 * n > q0 + 31) continue;

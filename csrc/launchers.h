@@ -8,14 +8,13 @@
 void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, void* s_out,
                    void* y, float* mean, float* rstd, int N, int d, float eps, bool rms,
                    uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
-                   hipStream_t st, bool r_planes = false);   // r_planes: r = fp32 split-K planes [2][N][d]
+                   hipStream_t st);
 // norm_fwd + the attention-dropout mask of (B, T, Hq) in one launch (horizontal fusion)
 void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void* b, void* s_out, void* y,
                         float* mean, float* rstd, int N, int d, float eps, bool rms, uint32_t thr16,
                         float drop_scale, const int64_t* seed, int64_t site, uint32_t* mask, int B, int T,
                         int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st,
-                        int g_begin = 0, int g_end = -1,    // tile groups [g_begin, g_end) of the mask
-                        bool r_planes = false);
+                        int g_begin = 0, int g_end = -1);   // tile groups [g_begin, g_end) of the mask
 int dltb_norm_bwd_partials(int N);
 void dltb_norm_bwd_dx(const void* dy, const void* s, const void* w, const float* mean,
                       const float* rstd, const void* dres, void* dx, int N, int d, bool rms,
@@ -33,8 +32,7 @@ int dltb_norm_bwd_fused_blocks(int N);
 bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
                          const float* rstd, const void* dres, void* dx, float* part, int N, int d,
                          bool rms, bool dxsum, hipStream_t st, void* dm = nullptr, uint32_t thr16 = 0,
-                         float drop_scale = 1.f, const int64_t* seed = nullptr, int64_t site = 0,
-                         bool dy_planes = false);   // dy = fp32 split-K planes [2][N][d]
+                         float drop_scale = 1.f, const int64_t* seed = nullptr, int64_t site = 0);
 
 // elementwise.hip
 void dltb_gelu_fwd(const void* f, void* g, long n, hipStream_t st);
@@ -151,17 +149,7 @@ int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* pa
               long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
               const float* alpha, hipStream_t st, int stages = 0);
 
-// ---- gemm_nt.hip: C[M,N] = A[M][K] B[N][K]^T (+bias) (+C), bf16, one workgroup per CU tile grid
-int dltb_gemm_nt_pick(int M, int N, int K);
-bool dltb_gemm_nt_supported(int M, int N, int K, int cfg);
-int dltb_gemm_nt_splits(int cfg);   // > 1: split-K config, writes fp32 planes part[split][M][N] instead of c
-// > 0: split-K pair-fixup config (bf16 c; part = fp32 [M * N] workspace, sync = this many zeroed ints)
-int dltb_gemm_nt_fixup_ints(int cfg, int M, int N);
-int dltb_gemm_nt(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,
-                 int N, int K, int accumulate, int cfg, int gm, hipStream_t st, float* part = nullptr,
-                 int* sync = nullptr);
-
-// ---- gemm_rs.hip: the same NT product with register-staged operands (the step's per-layer kernel)
+// ---- gemm_rs.hip: C[M,N] = A[M][K] B[N][K]^T (+bias) (+C), bf16, register-staged operands (the step's per-layer kernel)
 int dltb_gemm_rs_pick(int M, int N, int K);
 bool dltb_gemm_rs_supported(int M, int N, int K, int cfg);
 int dltb_gemm_rs(const void* a, const void* b, void* c, const void* bias, long lda, long ldb, long ldc, int M,

@@ -23,9 +23,7 @@ DLTB_DEV void norm_fwd_row(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ b, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int d, float eps,
-    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site, int row, int lane,
-    int rpl = 0) {
-  // rpl: r is two fp32 planes [2][N][d] (a split-K product, csrc/gemm_nt.hip) summed on the way in
+    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site, int row, int lane) {
   if (row >= N) return;
   const int nvec = d >> 3;
   const size_t base = (size_t)row * d;
@@ -55,16 +53,7 @@ DLTB_DEV void norm_fwd_row(
       unpack8(xv, v[j]);
       if (HAS_RES) {
         float rv[8];
-        if (rpl) {
-          const float* p0 = reinterpret_cast<const float*>(r) + base + idx * 8;
-          const float* p1 = p0 + (size_t)N * d;
-          const float4 a0 = ld16<float4>(p0), a1 = ld16<float4>(p0 + 4);
-          const float4 b0 = ld16<float4>(p1), b1 = ld16<float4>(p1 + 4);
-          rv[0] = a0.x + b0.x; rv[1] = a0.y + b0.y; rv[2] = a0.z + b0.z; rv[3] = a0.w + b0.w;
-          rv[4] = a1.x + b1.x; rv[5] = a1.y + b1.y; rv[6] = a1.z + b1.z; rv[7] = a1.w + b1.w;
-        } else {
-          unpack8(ld16<uint4>(r + base + idx * 8), rv);
-        }
+        unpack8(ld16<uint4>(r + base + idx * 8), rv);
         if (do_drop) {
 #pragma unroll
           for (int e = 0; e < 8; e += 2) {
@@ -130,9 +119,9 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ r, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ b, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int d, float eps,
-    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site, int rpl) {
+    uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site) {
   norm_fwd_row<NV, RMS, HAS_RES>(x, r, w, b, s_out, y, mean_out, rstd_out, N, d, eps, thr16, drop_scale,
-                                 seed_ptr, site, blockIdx.x * kWaves + (threadIdx.x >> 6), threadIdx.x & 63, rpl);
+                                 seed_ptr, site, blockIdx.x * kWaves + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
 // A block's first LayerNorm and its attention-dropout mask in ONE launch (horizontal fusion):
@@ -155,11 +144,11 @@ __global__ __launch_bounds__(256) void norm_fwd_mask_kernel(
     const bf16_t* __restrict__ b, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y,
     float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int d, float eps,
     uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr, int64_t site, int nb_norm,
-    MaskJob mj, int rpl) {
+    MaskJob mj) {
   const int bid = blockIdx.x;
   if (bid < nb_norm) {
     norm_fwd_row<NV, RMS, HAS_RES>(x, r, w, b, s_out, y, mean_out, rstd_out, N, d, eps, thr16, drop_scale,
-                                   seed_ptr, site, bid * kWaves + (threadIdx.x >> 6), threadIdx.x & 63, rpl);
+                                   seed_ptr, site, bid * kWaves + (threadIdx.x >> 6), threadIdx.x & 63);
   } else {
     const int m = bid - nb_norm;
     attn_mask_word(mj.mask, mj.T, mj.thr16, mj.seed, mj.site, (m % mj.gx) * 256 + threadIdx.x,
@@ -240,8 +229,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N, int d,
     int rpw, bf16_t* __restrict__ dm, uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr,
-    int64_t site, int dypl) {
-  // dypl: dy is two fp32 planes [2][N][d] (a split-K product) summed on the way in
+    int64_t site) {
   extern __shared__ __attribute__((aligned(16))) float fold[];   // [kFusedWaves][d]
   constexpr bool DXSUM = XS != 0;
   constexpr int K = (RMS ? 1 : 2) + (DXSUM ? 1 : 0);
@@ -279,16 +267,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
       const int idx = j * 64 + lane;
       if (idx < nvec) {
         float dyv[8], xv[8];
-        if (dypl) {
-          const float* p0 = reinterpret_cast<const float*>(dy) + base + idx * 8;
-          const float* p1 = p0 + (size_t)N * d;
-          const float4 a0 = ld16<float4>(p0), a1 = ld16<float4>(p0 + 4);
-          const float4 b0 = ld16<float4>(p1), b1 = ld16<float4>(p1 + 4);
-          dyv[0] = a0.x + b0.x; dyv[1] = a0.y + b0.y; dyv[2] = a0.z + b0.z; dyv[3] = a0.w + b0.w;
-          dyv[4] = a1.x + b1.x; dyv[5] = a1.y + b1.y; dyv[6] = a1.z + b1.z; dyv[7] = a1.w + b1.w;
-        } else {
-          unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
-        }
+        unpack8(ld16<uint4>(dy + base + idx * 8), dyv);
         unpack8(ld16<uint4>(s + base + idx * 8), xv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -447,10 +426,10 @@ template <bool RMS, bool HAS_RES>
 void launch_fwd_t(int nv, dim3 grid, hipStream_t st, const bf16_t* x, const bf16_t* r,
                   const bf16_t* w, const bf16_t* b, bf16_t* s_out, bf16_t* y, float* mean,
                   float* rstd, int N, int d, float eps, uint32_t thr, float scale,
-                  const int64_t* seed, int64_t site, int rpl) {
+                  const int64_t* seed, int64_t site) {
 #define DLTB_NF(NVV)                                                                             \
   hipLaunchKernelGGL((norm_fwd_kernel<NVV, RMS, HAS_RES>), grid, dim3(256), 0, st, x, r, w, b,   \
-                     s_out, y, mean, rstd, N, d, eps, thr, scale, seed, site, rpl)
+                     s_out, y, mean, rstd, N, d, eps, thr, scale, seed, site)
   switch (nv) {
     case 1: DLTB_NF(1); break;
     case 2: DLTB_NF(2); break;
@@ -475,9 +454,8 @@ int nv_for(int d) {
 void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, void* s_out,
                    void* y, float* mean, float* rstd, int N, int d, float eps, bool rms,
                    uint32_t thr16, float drop_scale, const int64_t* seed, int64_t site,
-                   hipStream_t st, bool r_planes) {
+                   hipStream_t st) {
   const int nv = nv_for(d);
-  const int rpl = r_planes ? 1 : 0;
   dim3 grid(cdiv(N, kWaves));
   auto X = (const bf16_t*)x;
   auto R = (const bf16_t*)r;
@@ -486,11 +464,11 @@ void dltb_norm_fwd(const void* x, const void* r, const void* w, const void* b, v
   auto S = (bf16_t*)s_out;
   auto Y = (bf16_t*)y;
   if (rms) {
-    if (r) launch_fwd_t<true, true>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, rpl);
-    else   launch_fwd_t<true, false>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, rpl);
+    if (r) launch_fwd_t<true, true>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site);
+    else   launch_fwd_t<true, false>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site);
   } else {
-    if (r) launch_fwd_t<false, true>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, rpl);
-    else   launch_fwd_t<false, false>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, rpl);
+    if (r) launch_fwd_t<false, true>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site);
+    else   launch_fwd_t<false, false>(nv, grid, st, X, R, W, B, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site);
   }
 }
 
@@ -498,11 +476,11 @@ template <bool RMS, bool HAS_RES>
 void launch_fwd_mask_t(int nv, int nb_norm, int nb_mask, hipStream_t st, const bf16_t* x, const bf16_t* r,
                        const bf16_t* w, const bf16_t* b, bf16_t* s_out, bf16_t* y, float* mean, float* rstd,
                        int N, int d, float eps, uint32_t thr, float scale, const int64_t* seed, int64_t site,
-                       const MaskJob& mj, int rpl) {
+                       const MaskJob& mj) {
   const dim3 grid(nb_norm + nb_mask);
 #define DLTB_NFM(NVV)                                                                                 \
   hipLaunchKernelGGL((norm_fwd_mask_kernel<NVV, RMS, HAS_RES>), grid, dim3(256), 0, st, x, r, w, b,   \
-                     s_out, y, mean, rstd, N, d, eps, thr, scale, seed, site, nb_norm, mj, rpl)
+                     s_out, y, mean, rstd, N, d, eps, thr, scale, seed, site, nb_norm, mj)
   switch (nv) {
     case 1: DLTB_NFM(1); break;
     case 2: DLTB_NFM(2); break;
@@ -518,9 +496,8 @@ void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void*
                         float* mean, float* rstd, int N, int d, float eps, bool rms, uint32_t thr16,
                         float drop_scale, const int64_t* seed, int64_t site, uint32_t* mask, int B, int T,
                         int Hq, uint32_t mask_thr16, const int64_t* mask_seed, int64_t mask_site, hipStream_t st,
-                        int g_begin, int g_end, bool r_planes) {
+                        int g_begin, int g_end) {
   const int nv = nv_for(d);
-  const int rpl = r_planes ? 1 : 0;
   const int ng = B * Hq * (T / kMaskKeyTile) * 2;          // tile groups of the whole mask
   if (g_end < 0 || g_end > ng) g_end = ng;
   const MaskJob mj{mask, T, mask_thr16, mask_seed, mask_site, cdiv(T, 256), g_begin};
@@ -533,11 +510,11 @@ void dltb_norm_fwd_mask(const void* x, const void* r, const void* w, const void*
   auto S = (bf16_t*)s_out;
   auto Y = (bf16_t*)y;
   if (rms) {
-    if (r) launch_fwd_mask_t<true, true>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj, rpl);
-    else   launch_fwd_mask_t<true, false>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj, rpl);
+    if (r) launch_fwd_mask_t<true, true>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
+    else   launch_fwd_mask_t<true, false>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
   } else {
-    if (r) launch_fwd_mask_t<false, true>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj, rpl);
-    else   launch_fwd_mask_t<false, false>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj, rpl);
+    if (r) launch_fwd_mask_t<false, true>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
+    else   launch_fwd_mask_t<false, false>(nv, nb_norm, nb_mask, st, X, R, W, Bi, S, Y, mean, rstd, N, d, eps, thr16, drop_scale, seed, site, mj);
   }
 }
 
@@ -612,7 +589,6 @@ struct FusedDrop {
   float scale;
   const int64_t* seed;
   int64_t site;
-  int dypl;           // dy as fp32 split-K planes
 };
 template <int NV, bool RMS, bool RES, int XS>
 void launch_bwd_fused(int N, int d, hipStream_t st, const bf16_t* dy, const bf16_t* s, const bf16_t* w,
@@ -621,7 +597,7 @@ void launch_bwd_fused(int N, int d, hipStream_t st, const bf16_t* dy, const bf16
   const int rpw = dltb_norm_bwd_fused_rpw(N);
   hipLaunchKernelGGL((norm_bwd_fused_kernel<NV, RMS, RES, XS>), dim3(dltb_norm_bwd_fused_blocks(N)),
                      dim3(kFusedWaves * 64), (size_t)kFusedWaves * d * sizeof(float), st, dy, s, w, mean, rstd, dres, dx,
-                     part, N, d, rpw, fd.dm, fd.thr16, fd.scale, fd.seed, fd.site, fd.dypl);
+                     part, N, d, rpw, fd.dm, fd.thr16, fd.scale, fd.seed, fd.site);
 }
 template <int NV, bool RMS, bool RES>
 void launch_bwd_fused_xs(int xs, int N, int d, hipStream_t st, const bf16_t* dy, const bf16_t* s,
@@ -643,7 +619,7 @@ void launch_bwd_fused_nv(bool res, int xs, int N, int d, hipStream_t st, const b
 bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const float* mean,
                          const float* rstd, const void* dres, void* dx, float* part, int N, int d,
                          bool rms, bool dxsum, hipStream_t st, void* dm, uint32_t thr16, float drop_scale,
-                         const int64_t* seed, int64_t site, bool dy_planes) {
+                         const int64_t* seed, int64_t site) {
   if (!dltb_norm_bwd_fused_supported(d)) return false;
   auto DY = (const bf16_t*)dy;
   auto S = (const bf16_t*)s;
@@ -652,7 +628,7 @@ bool dltb_norm_bwd_fused(const void* dy, const void* s, const void* w, const flo
   auto DX = (bf16_t*)dx;
   const bool res = dres != nullptr;
   const int xs = dm != nullptr ? 2 : (dxsum ? 1 : 0);
-  const FusedDrop fd{(bf16_t*)dm, thr16, drop_scale, seed, site, dy_planes ? 1 : 0};
+  const FusedDrop fd{(bf16_t*)dm, thr16, drop_scale, seed, site};
 #define DLTB_NBF(NVV)                                                                                    \
   do {                                                                                                   \
     if (rms) launch_bwd_fused_nv<NVV, true>(res, xs, N, d, st, DY, S, W, mean, rstd, DR, DX, part, fd);  \

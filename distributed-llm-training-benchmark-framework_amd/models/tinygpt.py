@@ -22,7 +22,6 @@ x1 = x + a; h2 = LN2(x1) (one fused kernel); f = h2 W1^T + b; g = GELU(f); m = g
 x2 = x1 + dropout(m).  GEMMs are hipBLASLt (torch), everything else is dltb._C on the GPU.
 """
 import math
-import os
 from types import SimpleNamespace
 
 import torch
@@ -157,9 +156,7 @@ class _BlockFn(torch.autograd.Function):
                 g, f = F_.gelu_fwd_grad(f, out=lb and lb.g)
             else:
                 g = F_.gelu_fwd(f, out=lb and lb.g)
-        m = F_.linear_fwd_splitk(g, w2, b2) if model.splitk_planes else None
-        if m is None:
-            m = F_.linear_fwd(g, w2, b2)    # Dropout(m) + x1 happens in the consumer's LayerNorm
+        m = F_.linear_fwd(g, w2, b2)        # Dropout(m) + x1 happens in the consumer's LayerNorm
         rt.release_forward(unit)
         ctx.model, ctx.i, ctx.lb = model, i, lb
         ctx.dgelu = dgelu                   # saved f is GELU'(f): the backward takes the dGELU-epilogue GEMM
@@ -208,9 +205,7 @@ class _BlockFn(torch.autograd.Function):
             df = F_.gelu_bwd(dg, f, s[9][0], s[9][1], red, out=lb and lb.df)
         wgrad(8, df, h2, ("df", "h2"))
         w1t = rt.weight_t(unit, 8, w1)
-        dh2 = F_.linear_dgrad_splitk(df, w1t) if model.splitk_planes else None
-        if dh2 is None:
-            dh2 = F_.linear_dgrad(df, w1, w1t)
+        dh2 = F_.linear_dgrad(df, w1, w1t)
         dx1 = F_.norm_bwd(dh2, x1, ln2w, mean2, rstd2, dx2, s[6][0], s[7][0], s[6][1], False,
                           red, bias=("dx", s[5][0], s[5][1]), dx_out=lb and lb.dx1)
         # attention
@@ -222,9 +217,7 @@ class _BlockFn(torch.autograd.Function):
                     1.0 / math.sqrt(d // H), False, p, rt.seed, model.site_attn(i))
         wgrad(2, dqkv, h1, ("dqkv", "h1"))
         wint = rt.weight_t(unit, 2, win)
-        dh1 = F_.linear_dgrad_splitk(dqkv, wint) if model.splitk_planes else None
-        if dh1 is None:
-            dh1 = F_.linear_dgrad(dqkv, win, wint)
+        dh1 = F_.linear_dgrad(dqkv, win, wint)
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False,
                          red, bias=(dqkv, s[3][0], s[3][1]))
         if shared is None:
@@ -315,9 +308,6 @@ class TinyGPT(nn.Module):
         # each attention-dropout mask is generated in two halves, beside the previous block's LN2
         # and beside this block's LN1 (both latency-bound row norms that leave VALU issue idle)
         self.mask_split = True         # (attribute, not an env switch: tests compare both paths)
-        # fc2 forward and the fc1 / qkv data gradients as split-K fp32 planes read by the consuming
-        # LayerNorm kernels (ops/functional.py linear_fwd_splitk); A/B switch, default off
-        self.splitk_planes = os.environ.get("DLTB_SPLITK_PLANES", "0") == "1"
         self._next_amask = None
         self._build_units()
 
@@ -336,20 +326,19 @@ class TinyGPT(nn.Module):
     def _build_units(self):
         t = self.transformer
         # the tied token table (wte = lm_head.weight) is the head unit's third parameter: the head's
-        # backward, the first of the step, completes its dense gradient (see _EmbedFn).
-        # DLTB_TIE_IN_HEAD=0 (A/B only) keeps it in the embedding unit, reduced after the last
-        # backward op as before round 3.
-        tie_in_head = os.environ.get("DLTB_TIE_IN_HEAD", "1") == "1"
+        # backward, the first of the step, completes its dense gradient (see _EmbedFn), so engines reduce
+        # it right after the head instead of after the last backward op (round 3: emulated DDP N = 8
+        # exposed comm 2.01 -> 1.27 ms, profiles/emulated_ab_tail_tie_r3.txt)
         wpe = [("transformer.wpe.weight", t["wpe"].weight)]
         wte = [("transformer.wte.weight", t["wte"].weight)]
-        self.unit_embed = Unit("embed", wpe if tie_in_head else wte + wpe, 0)
+        self.unit_embed = Unit("embed", wpe, 0)
         self.unit_blocks = [Unit(f"h.{i}", [(f"transformer.h.{i}.{n}", p) for n, p in blk.param_list()], i + 1)
                             for i, blk in enumerate(t["h"])]
         self.unit_head = Unit("head", [("transformer.ln_f.weight", t["ln_f"].weight),
-                                       ("transformer.ln_f.bias", t["ln_f"].bias)] + (wte if tie_in_head else []),
+                                       ("transformer.ln_f.bias", t["ln_f"].bias)] + wte,
                               len(self.unit_blocks) + 1)
-        self.tok_slot = (self.unit_head, 2) if tie_in_head else (self.unit_embed, 0)
-        self.pos_slot = (self.unit_embed, 0) if tie_in_head else (self.unit_embed, 1)
+        self.tok_slot = (self.unit_head, 2)
+        self.pos_slot = (self.unit_embed, 0)
 
     def units(self):
         """Units in forward order (the engines reverse it for backward-ordered buckets)."""

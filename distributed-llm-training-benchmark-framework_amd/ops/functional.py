@@ -30,21 +30,9 @@ def _into(out, t):
     return out
 
 
-def is_planes(t):
-    """A split-K product's two fp32 planes [2, rows, d] (linear_fwd_splitk / linear_dgrad_splitk), which
-    the norm kernels sum on the way in, in place of a bf16 [rows, d] operand."""
-    return t is not None and t.dim() == 3 and t.shape[0] == 2 and t.dtype == torch.float32
-
-
-def _unplane(t, like):
-    return t.sum(0).to(like.dtype) if is_planes(t) else t
-
-
 def norm_fwd(x, r, w, b, eps, rms, p=0.0, seed=None, site=0, y_out=None):
     """Returns (s, y, mean, rstd); s = x + dropout(r) when r is given (else None).  ``y_out``: write
-    y into this (layer-strided activation buffer) view.  ``r`` may be split-K planes (GPU)."""
-    if not _gpu(x):
-        r = _unplane(r, x)
+    y into this (layer-strided activation buffer) view."""
     if _gpu(x):
         s, y, mean, rstd = ext().norm_fwd(x, r, w, b, eps, rms, p, _sd(seed) if p > 0 else None, site, y_out)
         return (s if r is not None else None), y, (None if rms else mean), rstd
@@ -67,8 +55,6 @@ def norm_fwd_mask(x, r, w, b, eps, rms, p, seed, site, y_out, B, T, Hq, p_attn, 
         s_, y, mean, rstd, mask = ext().norm_fwd_mask(x, r, w, b, eps, rms, p, seed.device_tensor, site, y_out,
                                                       B, T, Hq, p_attn, attn_site, mask_out, g0, g1)
         return (s_ if r is not None else None), y, (None if rms else mean), rstd, mask
-    if is_planes(r) and not _gpu(x):
-        r = _unplane(r, x)
     s_, y, mean, rstd = norm_fwd(x, r, w, b, eps, rms, p, seed, site, y_out)
     return s_, y, mean, rstd, (attn_mask(B, T, Hq, p_attn, seed, attn_site, x) if part is None else None)
 
@@ -128,11 +114,7 @@ def norm_bwd(dy, s, w, mean, rstd, dres, gw, gb, accumulate, rms, red=None, bias
 
     ``drop=(p, seed, site, dm_out, db, db_acc)``: also return dm = Dropout_backward(dx) of dropout
     site ``site`` with its column sum into ``db`` -- ``(dx, dm)`` -- fused into the same kernel on
-    the GPU (the previous block's MLP dropout and fc2 bias gradient).
-
-    ``dy`` may be split-K planes: read by the fused GPU kernel, summed to bf16 for the other paths."""
-    if is_planes(dy) and not (red is not None and _gpu(s) and ext().norm_bwd_fused_supported(s.shape[-1])):
-        dy = _unplane(dy, s)
+    the GPU (the previous block's MLP dropout and fc2 bias gradient)."""
     if drop is not None:
         dp, dseed, dsite, dm_out, db, db_acc = drop
         if red is not None and _gpu(dy) and ext().norm_bwd_fused_supported(dy.shape[-1]):
@@ -529,42 +511,6 @@ def linear_fwd(x2d, w, b=None):
     if b is None:
         return torch.mm(x2d, w.t())
     return torch.addmm(b, x2d, w.t())
-
-
-# Split-K NT products as two fp32 planes (csrc/gemm_nt.hip cfg 7: 128 x 128 tiles, 2 K-splits) for the
-# K-long products whose only consumer is a norm kernel that can sum the planes on its way in -- fc2
-# forward (-> the next LN1 / ln_f residual) and the fc1 / qkv data gradients (-> the LN2 / LN1
-# backward).  A/B switch: DLTB_SPLITK_PLANES (models/tinygpt.py); shapes outside the measured family
-# (N <= 1024 output columns, K >= 2048) keep hipBLASLt.
-_SPLITK_CFG = 7
-splitk_calls = 0          # products issued as planes (tests check that the path ran)
-
-
-def _splitk_ok(a, b):
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and a.dim() == 2):
-        return False
-    M, K = a.shape
-    N = b.shape[0]
-    return N <= 1024 and K >= 2048 and a.stride(1) == 1 and b.is_contiguous() and \
-        ext().gemm_nt_supported(M, N, K, _SPLITK_CFG)
-
-
-def linear_fwd_splitk(x2d, w, b=None):
-    """x W^T (+ b) as split-K planes [2, M, N] (bias in plane 0), or None."""
-    global splitk_calls
-    if not _splitk_ok(x2d, w):
-        return None
-    splitk_calls += 1
-    return ext().gemm_nt(x2d, w, None, b, False, _SPLITK_CFG, 4)
-
-
-def linear_dgrad_splitk(dy2d, wt):
-    """dY W = dY (W^T)^T as split-K planes from the cached contiguous W^T, or None."""
-    global splitk_calls
-    if wt is None or not _splitk_ok(dy2d, wt):
-        return None
-    splitk_calls += 1
-    return ext().gemm_nt(dy2d, wt, None, None, False, _SPLITK_CFG, 4)
 
 
 def linear_dgrad(dy2d, w, wt=None):

@@ -43,9 +43,6 @@ from .flat import ALIGN, owner_segments, plan_layout
 from .wgrad import WgradQueue
 
 
-_SPARSE_DEFER = os.environ.get("DLTB_SPARSE_DEFER", "1") == "1"
-
-
 def _dtype_name(dt):
     return {torch.bfloat16: "bf16", torch.float16: "fp16", torch.float32: "fp32"}.get(dt, str(dt))
 
@@ -86,7 +83,7 @@ class ReplicatedEngine(Engine):
         # rounded up to a multiple of 4 of the model's repeated unit (64 MiB -> 4 blocks, 101 MB).
         # Only the embedding (the unit that finishes last) then keeps a bucket of its own: a solo block 0
         # would be a 1-block batch (110 us) and leave 3 blocks for the group before it.
-        mult = int(cfg.extra.get("bucket_unit_multiple", os.environ.get("DLTB_BUCKET_UNIT_MULTIPLE", 4)))
+        mult = int(cfg.extra.get("bucket_unit_multiple", 4))
         solo_tail, solo_head = 2, 0
         if self.world > 1 and self.defer_wgrad and bucket_elems > 0 and mult > 1:
             sizes = sorted(u.numel for u in units)
@@ -96,7 +93,7 @@ class ReplicatedEngine(Engine):
             # the head (the tied 65.5 MB token table at TinyGPT-A) is a bucket of its own: otherwise it
             # shares the first bucket with two blocks and the blocks' dW batches come out 2/4/4/4/2
             # (a 2-block batch costs 75 us per block against 58 for 4, profiles/wgrad_batch_size_r2.txt)
-            solo_head = int(cfg.extra.get("solo_head_units", os.environ.get("DLTB_SOLO_HEAD", 1)))
+            solo_head = int(cfg.extra.get("solo_head_units", 1))
             if self._ddp_pipe_wanted() or cfg.extra.get("shard_optimizer"):
                 # DDP with the optimizer pipelined per bucket: the last bucket's all-reduce is the exposed
                 # tail, so blocks 0 and 1 get buckets of their own (1-block dW batches, +~0.1 ms) and the
@@ -107,18 +104,18 @@ class ReplicatedEngine(Engine):
         # the first bucket(s) after the head: twice the size (fewer collectives early in the backward,
         # while compute hides them; the buckets at its end -- the first parameter all-gathers of the
         # next forward -- keep the usual size): emulated ZeRO-2 N = 8 -0.7 %, N = 2 -0.5 %
-        # (profiles/emulated_ab_early_bucket_r4.txt).  DLTB_EARLY_BUCKETS (count; 0 = off).
+        # (profiles/emulated_ab_early_bucket_r4.txt).  cfg.extra["early_buckets"] (count; 0 = off).
         # (ZeRO-2 only: DDP and ZeRO-1 wait for every bucket before the optimizer of the same
         # micro-step / window, and there a later first collective only lengthens the exposed tail --
         # DDP fp16 with fp32 all-reduce N = 8 63.6 -> 60.3 %, profiles/emulated_ab_early_bucket_r4.txt)
-        early = int(cfg.extra.get("early_buckets", os.environ.get("DLTB_EARLY_BUCKETS", 1))) \
+        early = int(cfg.extra.get("early_buckets", 1)) \
             if (self.world > 1 and bucket_elems > 0 and self.stage == 2) else 0
         shard = self.stage >= 1
         self.layout = L = plan_layout(units, self.world, bucket_elems, ALIGN, shard=shard,
                                       solo_tail=int(cfg.extra.get("solo_tail_units",
-                                                                  os.environ.get("DLTB_SOLO_TAIL", solo_tail))),
+                                                                  solo_tail)),
                                       bucket_max=ds_cap, solo_head=solo_head,
-                                      early_elems=int(os.environ.get("DLTB_EARLY_MULT", 2)) * bucket_elems
+                                      early_elems=2 * bucket_elems
                                       if early else 0, early_count=early)
         # DeepSpeed switches (zero2.json; all true there and by default): overlap_comm false waits
         # for every collective where it is issued; reduce_scatter false all-reduces each bucket and
@@ -177,21 +174,9 @@ class ReplicatedEngine(Engine):
         # norm: both keep the whole-model update after the last wait.)
         self._ddp_pipe = self._ddp_pipe_wanted()
         self._ar_works = {}      # bucket -> its all-reduce (untracked) while the pipeline is on
-        # A/B (DLTB_DDP_EARLY_OPT=1; off by default): at world > 1 on the GPU, a bucket's AdamW segment
-        # runs on a side stream as soon as its all-reduce lands, i.e. under the rest of the backward
-        # instead of after it.  A reduced bucket's parameters are not read again by this backward (its
-        # blocks' dgrad / dW ran before the all-reduce was issued); the next forward waits for the side
-        # stream; the tied token table's bucket stays last (its gathered rows).  Measured slower: the
-        # emulated ddp_bf16 N = 8 step 10.07 -> 10.25 ms with full grids, 10.27 / 10.69 / 12.5 ms with
-        # the update capped at 128 / 64 / 32 workgroups (profiles/ddp_early_update_ab_r5.txt) -- the
-        # backward's kernels lose more to the co-running update than the tail gains.
-        self._early_opt = (self._ddp_pipe and self.device.type == "cuda"
-                           and os.environ.get("DLTB_DDP_EARLY_OPT", "0") == "1")
-        self._opt_stream = torch.cuda.Stream(self.device) if self._early_opt else None
-        # workgroups of each early update (0: one per table row): a capped grid leaves the CUs to the
-        # backward's kernels and trickles the update beside them
-        self._early_grid = int(os.environ.get("DLTB_DDP_EARLY_GRID", 0))
-        self._early = None       # this step's early-update state: {"done": set, "gscale": t} or None
+        # (a bucket's update on a side stream right behind its all-reduce, under the rest of the backward,
+        # measured slower -- emulated ddp_bf16 N = 8 10.07 -> 10.25 ms, profiles/ddp_early_update_ab_r5.txt --
+        # and was removed in round 6)
         if self._ddp_pipe:
             g_full = self.comm_f32 if self.comm_f32 is not None else self.flat_grad
             opt_segs = [(bk.start, bk.end - bk.start, self.flat_param[bk.start:bk.end]) for bk in L.buckets]
@@ -205,15 +190,6 @@ class ReplicatedEngine(Engine):
         self._pending = [len(b.units) for b in L.buckets]
         self._bucket_of = L.unit_bucket
         self._wq = WgradQueue()
-        # A/B (DLTB_WGRAD_SIDE = G blocks, 0 = off): at world 1 the window's batched dW of every G
-        # blocks whose backward has finished is issued on a side stream, beside the rest of the dX
-        # chain (whose per-layer GEMMs run one tile per CU and leave MFMA idle), instead of all 16
-        # blocks after it; the main stream joins the side stream at the end of the backward
-        self._side_group = int(os.environ.get("DLTB_WGRAD_SIDE", 0)) if (
-            self.world == 1 and dev.type == "cuda" and self.defer_wgrad) else 0
-        self._wgrad_stream = torch.cuda.Stream(dev) if self._side_group > 0 else None
-        self._side_units = []    # reported units whose queued dW waits for a side-stream batch
-        self._side_hold = []     # their operands, alive until the join (the main stream may free them)
         # Window-wide weight gradients: where no collective reads a gradient before the window ends
         # (world 1, or the window-reduced ZeRO-1 / DDP paths), the model keeps every micro-step's
         # dW operands and the window's dW = sum_m dY_m^T X_m runs at its last micro-step as one
@@ -251,7 +227,7 @@ class ReplicatedEngine(Engine):
         # exchanges its rows.  2048 rows scattered locally instead of an all-gather of world x 2048
         # rows + ids and a sort-path scatter every micro-step.
         self._carry_on = (self._tail_defer and
-                          bool(cfg.extra.get("carry_token_rows", os.environ.get("DLTB_CARRY_ROWS", "1") == "1")))
+                          bool(cfg.extra.get("carry_token_rows", True)))
         self._carry = None       # (token slot, rows, ids) waiting for the next micro-step's head
         nbytes = L.total * (4 if self.comm_f32 is not None else elem)
         if self.world > 1:
@@ -308,10 +284,6 @@ class ReplicatedEngine(Engine):
 
     def grads_ready(self, unit):
         self._reported.add(id(unit))
-        if self._side_group and self._wq.has([unit]):
-            self._side_units.append(unit)
-            if len(self._side_units) >= self._side_group:
-                self._side_flush()
         if self._carry is not None and self._carry[0][0] is unit:
             self._apply_carry()
         b = self._bucket_of.get(id(unit))
@@ -428,8 +400,6 @@ class ReplicatedEngine(Engine):
                 g = c
             if self._ddp_pipe:       # waited by its own AdamW segment (or the token rows), not wait_all
                 self._ar_works[b] = self.comm.all_reduce(g, async_op=True, track=False)
-                if self._early_opt and self._is_boundary:
-                    self._launch_early(b)
             else:
                 self.comm.all_reduce(g, async_op=not sync)
         elif not self._use_rs:
@@ -489,21 +459,9 @@ class ReplicatedEngine(Engine):
         if self.stage == 2 and self.world > 1:
             self._written.clear()         # the full gradient buffer is reduced every micro-step
 
-    def _side_flush(self):
-        units, self._side_units = self._side_units, []
-        self._side_hold.extend(self._wq.pending(units))
-        self._wgrad_stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self._wgrad_stream):
-            self._wq.flush(units)
-
     def _finish_backward(self):
         if self._red is not None:
             self._red.flush()
-        if self._side_hold or self._side_units:
-            self._side_units = []
-            self._wq.flush()                                    # what did not fill a side batch
-            torch.cuda.current_stream(self.device).wait_stream(self._wgrad_stream)
-            self._side_hold = []
         self._wq.flush()                                        # world 1: every block in one batch
         self._zero_unreported()
         if self._reduce_now():
@@ -520,7 +478,7 @@ class ReplicatedEngine(Engine):
         # table's own AdamW segment, which it runs last.)
         pipe_rows = self._ddp_pipe and self._is_boundary
         if self._sparse is not None and not pipe_rows and \
-                not (self._tail_defer and not self._is_boundary and _SPARSE_DEFER):
+                not (self._tail_defer and not self._is_boundary):
             b = self._bucket_of[id(self._sparse[0][0])]
             if b in self._rs_inflight:
                 self._drain_bucket(b)          # the token table's chunk, then its sparse rows
@@ -553,33 +511,11 @@ class ReplicatedEngine(Engine):
         cfg = self.cfg
         return (int(cfg.zero_stage) == 0 and self.world > 1 and bool(cfg.extra.get("overlap_comm", True))
                 and self.scaler is None and not cfg.grad_clip > 0 and not cfg.extra.get("track_grad_norm", False)
-                and os.environ.get("DLTB_DDP_OPT_PIPELINE", "1") == "1")
+                and bool(cfg.extra.get("ddp_opt_pipeline", True)))
 
     def _tied_bucket(self):
         tu = getattr(self.model, "tok_slot", (None,))[0]
         return self._bucket_of.get(id(tu)) if tu is not None else None
-
-    def _launch_early(self, b):
-        """AdamW of bucket ``b`` on the side stream, behind its all-reduce (see ``_early_opt``)."""
-        from ..comm.collectives import _EmuWork
-        w = self._ar_works.get(b)
-        if b == self._tied_bucket() or w is None:
-            return
-        if not (isinstance(w, _EmuWork) or type(w).__module__.startswith("torch")):
-            return                               # lazy / host-staged works run their copies at wait()
-        if self._early is None:                  # first early bucket of this step: lr, hp, coefficient
-            g = self._owner_grad()
-            self.opt.prepare(self.sched(self.opt_steps))
-            gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)
-            ev = torch.cuda.Event()
-            ev.record()
-            self._early = {"done": set(), "gscale": gscale, "ev": ev}
-        g = self._owner_grad()
-        with torch.cuda.stream(self._opt_stream):
-            self._opt_stream.wait_event(self._early["ev"])
-            self._ar_works.pop(b).wait()         # this stream waits for the all-reduce
-            self.opt.launch_segment(b, g, self._early["gscale"], grid_cap=self._early_grid)
-        self._early["done"].add(b)
 
     def _wait_allreduce(self, b):
         w = self._ar_works.pop(b, None)
@@ -592,33 +528,25 @@ class ReplicatedEngine(Engine):
             # the tied token table's bucket goes last: its gathered token rows (issued after every
             # all-reduce) are scatter-added into it first
             g = self._owner_grad()
-            early, self._early = self._early, None
-            if early is None:
-                gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)   # (no clip: a fill)
-                self.opt.prepare(lr)
-            else:                                # lr / hp / coefficient already set by _launch_early
-                gscale = early["gscale"]
+            gscale = self._clip_coef([g], 1.0 / (self.world * self.accum), False)   # (no clip: a fill)
+            self.opt.prepare(lr)
             order = list(range(len(self.layout.buckets)))
             bt = self._bucket_of[id(self._sparse[0][0])] if self._sparse is not None else None
             if bt is not None:
                 order.remove(bt)
                 order.append(bt)
             for b in order:
-                if early is not None and b in early["done"]:
-                    continue
                 self._wait_allreduce(b)
                 if b == bt:
                     self._apply_sparse()
                 self.opt.launch_segment(b, g, gscale)
-            if early is not None:
-                torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
             return
         self._apply_update(self._owner_grad(), lr, 1.0 / (self.world * self.accum), sharded=self.stage >= 1)
 
     def _deferred_optimizer_step(self, lr):
         g = self._owner_grad()
         if (self._use_ag and self.scaler is None and g.is_cuda and not self.opt.sub_group
-                and os.environ.get("DLTB_OPT_PIPELINE", "1") == "1"):
+                and bool(self.cfg.extra.get("opt_pipeline", True))):
             # clip coefficient once, then per bucket (gather order): its AdamW rows, then its
             # all-gather -- the all-gather of the tied table's bucket starts after that bucket's
             # update instead of after the whole shard's, and every later one earlier by the rest
@@ -651,8 +579,6 @@ class ReplicatedEngine(Engine):
         order = list(reversed(range(len(self.layout.buckets))))
         tu = getattr(self.model, "tok_slot", (None,))[0]
         bt = self._bucket_of.get(id(tu)) if tu is not None else None
-        if os.environ.get("DLTB_AG_TIED_FIRST", "1") != "1":     # (A/B: the old plain forward order)
-            bt = None
         if bt is not None and bt in order:
             order.remove(bt)
             order.insert(0, bt)

@@ -165,8 +165,7 @@ class ShardedEngine(Engine):
         # stage3_max_live_parameters (DeepSpeed's release rule), instead of released and re-gathered
         self._prefetch_elems = int(cfg.extra.get("prefetch_elems", 0)) if cfg.zero_stage == 3 else 0
         tu = getattr(self.model, "tok_slot", (None,))[0]
-        self._tied_group = self._group_of.get(id(tu)) if (tu is not None and self.world > 1 and
-                                                          os.environ.get("DLTB_AG_TIED_FIRST", "1") == "1") else None
+        self._tied_group = self._group_of.get(id(tu)) if (tu is not None and self.world > 1) else None
         self._reuse_keep = set()
         if cfg.zero_stage == 3 and not self.keep_all and cfg.max_reuse_distance:
             after = 0
@@ -203,7 +202,7 @@ class ShardedEngine(Engine):
         # host time per acquire, 36 acquires per FSDP micro-step)
         self._view_cache = {}
         self._gpool = {}             # numel -> free gathered buffers (returned by _release)
-        self._pool_on = os.environ.get("DLTB_GATHER_POOL", "1") == "1"      # A/B toggle
+        self._pool_on = bool(cfg.extra.get("gather_pool", True))
         self._gviews = {}            # (id(unit), i) -> (gradient slot view, its group or None)
         # resident group gradient buffers at world > 1 for models below 2B parameters (a full model's
         # worth of bf16 gradients per rank: 0.47 GB at TinyGPT-A; Mistral-7B keeps transient ones):
@@ -215,7 +214,7 @@ class ShardedEngine(Engine):
         # head-group gradient instead of exchanged (as the replicated engines do; the window's sum is
         # unchanged); only the window's last micro-step exchanges them
         self._carry_on = (self.world > 1 and self.accum > 1 and
-                          bool(cfg.extra.get("carry_token_rows", os.environ.get("DLTB_CARRY_ROWS", "1") == "1")))
+                          bool(cfg.extra.get("carry_token_rows", True)))
         self._carry = None
         # single process: the dW products of all blocks run as strided-batched GEMMs at the end of
         # backward (parallel/wgrad.py).  World > 1 with resident gradient buffers: the groups'
@@ -225,7 +224,7 @@ class ShardedEngine(Engine):
         # dW product costs 110 us per TinyGPT-A block against 58 for 4 batched,
         # profiles/wgrad_batch_size_r2.txt); otherwise the products are issued immediately
         batch = bool(cfg.extra.get("batch_wgrad", os.environ.get("DLTB_BATCH_WGRAD", "1") == "1"))
-        self._group_batch = int(cfg.extra.get("group_wgrad_batch", os.environ.get("DLTB_GROUP_WGRAD_BATCH", 4)))
+        self._group_batch = int(cfg.extra.get("group_wgrad_batch", 4))
         self._arena = None
         if self.world > 1 and self._grad_resident and batch and self._group_batch > 1:
             self._arena = torch.empty(sum(g.total for g in self._order), dtype=dt, device=dev)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fused AdamW launch time at TinyGPT-A size (236.4M fp32 master / moments, bf16 gradient and parameter copy).
 
-    python scripts/bench_adamw.py [--n 236406784] [--iters 20]      (DLTB_ADAM_WIDE=1: the 16-byte path, DLTB_ADAM_T128=1: 128-lane blocks)
+    python scripts/bench_adamw.py [--n 236406784] [--iters 20]
 
 Bytes moved per element: read master, m, v (12) + bf16 grad (2), write master, m, v (12) + bf16 param (2)."""
 import argparse
@@ -38,5 +38,5 @@ for _ in range(a.iters):
     ts.append(s.elapsed_time(e) * 1e3)
 ts.sort()
 med = ts[len(ts) // 2]
-print(f"adamw n={n} wide={os.environ.get('DLTB_ADAM_WIDE', '0')} t128={os.environ.get('DLTB_ADAM_T128', '0')}: median {med:.1f} us, min {ts[0]:.1f} us, "
+print(f"adamw n={n}: median {med:.1f} us, min {ts[0]:.1f} us, "
       f"{28 * n / med / 1e6:.2f} TB/s (28 B/elem)", flush=True)

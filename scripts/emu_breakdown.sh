@@ -13,5 +13,4 @@ run w1 DLTB_X=0 && \
 EXTRA="--emulate 8 --host-check" run e8_fast DLTB_EMU_ALPHA_US=0 DLTB_EMU_BUS_GBPS=1e9 && \
 EXTRA="--emulate 8" run e8_ch1 DLTB_EMU_CHANNELS=1 && \
 EXTRA="--emulate 8" run e8_ch32 DLTB_EMU_CHANNELS=32 && \
-EXTRA="--emulate 8" run e8_ch32_solo DLTB_BUCKET_UNIT_MULTIPLE=1 DLTB_SOLO_TAIL=2 && \
 EXTRA="--emulate 8 --graphs on" run e8_graphs DLTB_GRAPHS=1

@@ -30,12 +30,18 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--timeout", type=int, default=900)
+    ap.add_argument("--cases", default=None, help="comma-separated multirank_check.py cases (default: all)")
+    ap.add_argument("--seq-len", type=int, default=None)
     a = ap.parse_args()
     ref_batch = 1
     for w in a.ws:                      # every world size must divide the global rows
         while ref_batch % w:
             ref_batch += 1
     extra = ("--ref-batch", str(ref_batch))
+    if a.cases:
+        extra += ("--cases", a.cases)
+    if a.seq_len:
+        extra += ("--seq-len", str(a.seq_len))
     env = {k: v for k, v in os.environ.items() if k not in ("DLTB_COMM", "DLTB_COMM_LAZY")}
     verdict, ok = {"ref_batch": ref_batch, "device": a.device, "world_sizes": {}}, True
     with tempfile.TemporaryDirectory() as d:

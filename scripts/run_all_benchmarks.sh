@@ -7,6 +7,8 @@
 #  1. xGMI collective sweep (scripts/bench_collectives.py) at every multi-GPU world size ->
 #     summary/xgmi_buckets.json (and profiles/xgmi_buckets.json on real GPUs), which
 #     comm/topology.py reads to size the gradient buckets of every following run.
+#  1b. RCCL transport A/B on the flagship at the largest world size (NCCL_MIN_NCHANNELS 16 / 32, stream
+#      priority) -> summary/transport_ab.jsonl (TRANSPORT_AB=0 skips it).
 #  2. Each config: launch (torchrun) -> collect -> failure bookkeeping.  Rows (STRATS):
 #       ddp fsdp zero2 zero3      the reference's four strategies, reference semantics and precision
 #                                 (DDP / FSDP: fp16 + dynamic loss scaling, DDP fp32 all-reduce;
@@ -22,6 +24,7 @@
 #      trainable_params and per-rank peak HBM land in each row's .extended.json sidecar.
 #      M7B=0 skips it; M7B_TIER / M7B_SEQ / M7B_STEPS override (the CPU rehearsal uses mtiny).
 #  3. parse -> plot -> report.
+#  4. summary/first_multigpu_report.md (scripts/first_multigpu_report.py).
 # Like the reference it always exits 0; failed configs are listed in results/summary/failures.json.
 #
 #   ./scripts/run_all_benchmarks.sh [results-dir]
@@ -48,13 +51,15 @@ echo "  MI355X Distributed Training Benchmark Suite ($NGPU GPUs visible)"
 echo "=================================================================="
 
 # ---- 0. RCCL correctness: every engine at N ranks == 1 rank on the concatenated batch
-if [[ "${RCCL_CHECK:-1}" != "0" && -z "${FORCE_NPROC:-}" && "$NGPU" -ge 2 ]]; then
+#      (FORCE_NPROC rehearsal: gloo on the CPU, two cases at a short sequence)
+if [[ "${RCCL_CHECK:-1}" != "0" && "$NGPU" -ge 2 ]]; then
   RWS=(); for ws in $WS_LIST; do [[ "$ws" -ge 2 && "$ws" -le "$NGPU" ]] && RWS+=("$ws"); done
   if [[ ${#RWS[@]} -gt 0 ]]; then
     CHK=("${RWS[0]}"); [[ ${#RWS[@]} -gt 1 ]] && CHK+=("${RWS[-1]}")
+    RX=(); [[ -n "${FORCE_NPROC:-}" ]] && RX=(--device cpu --cases ddp,zero2 --seq-len 64)
     echo "---- RCCL equivalence ws=${CHK[*]}"
     timeout -k 30 "$((3 * TIMEOUT))" python3 "$ROOT/scripts/rccl_equivalence.py" --ws "${CHK[@]}" \
-      --out "$RESULTS/summary/rccl_equivalence.json" > "$RESULTS/rccl_equivalence.log" 2>&1 \
+      ${RX[@]+"${RX[@]}"} --out "$RESULTS/summary/rccl_equivalence.json" > "$RESULTS/rccl_equivalence.log" 2>&1 \
       || { FAILED+=("rccl-equivalence"); echo "     FAILED (see $RESULTS/rccl_equivalence.log)"; }
   fi
 fi
@@ -85,6 +90,35 @@ if worlds:
         shutil.copyfile(out, repo_copy)
 PY
   [[ -f "$PROFILE" ]] && export DLTB_XGMI_PROFILE="$PROFILE"
+fi
+
+# ---- 1b. RCCL transport knobs on the flagship (ZeRO-2, bench.py) at the largest multi-GPU world size:
+#      default, NCCL_MIN_NCHANNELS=16 / 32, the RCCL stream at normal priority -> summary/transport_ab.jsonl
+#      (one bench.py JSON line per variant, with a "transport" field; TRANSPORT_AB=0 skips it)
+if [[ "${TRANSPORT_AB:-1}" != "0" ]]; then
+  TWS=0; for ws in $WS_LIST; do [[ "$ws" -ge 2 && "$ws" -le "$NGPU" && "$ws" -gt "$TWS" ]] && TWS=$ws; done
+  if [[ "$TWS" -ge 2 ]]; then
+    if [[ -n "${FORCE_NPROC:-}" ]]; then BX=(--device cpu --tier "$TIER" --seq-len "$SEQ" --steps 6 --warmup 5)
+    else BX=(--steps "${TRANSPORT_STEPS:-20}" --warmup 5); fi
+    : > "$RESULTS/summary/transport_ab.jsonl"
+    for knob in default NCCL_MIN_NCHANNELS=16 NCCL_MIN_NCHANNELS=32 DLTB_COMM_HIGH_PRIORITY=0; do
+      echo "---- transport ws=$TWS $knob"
+      KV=(); [[ "$knob" != default ]] && KV=("$knob")
+      tlog="$RESULTS/transport_${knob//=/_}.log"
+      if timeout -k 30 "$TIMEOUT" env ${KV[@]+"${KV[@]}"} python3 "$ROOT/bench.py" --gpus "$TWS" --strategy zero2 \
+           "${BX[@]}" > "$tlog" 2>&1; then
+        python3 - "$tlog" "$knob" "$RESULTS/summary/transport_ab.jsonl" <<'PY' || FAILED+=("transport-$knob")
+import json, sys
+log, knob, out = sys.argv[1:4]
+rec = [json.loads(l) for l in open(log) if l.startswith("{")][-1]
+rec["transport"] = knob
+open(out, "a").write(json.dumps(rec) + "\n")
+PY
+      else
+        FAILED+=("transport-$knob"); echo "     FAILED (see $tlog)"
+      fi
+    done
+  fi
 fi
 
 # ---- 2. benchmark matrix
@@ -161,5 +195,9 @@ PY
 python3 "$ROOT/scripts/parse_metrics.py" --results-dir "$RESULTS" --out "$RESULTS/summary" \
   && python3 "$ROOT/scripts/plot.py" --results "$RESULTS/summary/metrics.csv" --out "$RESULTS/summary/plots" \
   && python3 "$ROOT/scripts/make_report.py" --csv "$RESULTS/summary/metrics.csv" --out "$RESULTS/summary"
+# ---- 4. the multi-GPU summary: measured curve, error of the shipped emulated-fabric prediction per row, the
+#      fitted alpha-beta per world size and collective, the transport A/B, the RCCL equivalence verdict
+python3 "$ROOT/scripts/first_multigpu_report.py" --results "$RESULTS" \
+  --out "$RESULTS/summary/first_multigpu_report.md" || echo "first_multigpu_report failed"
 echo "completed: $DONE, failed: ${#FAILED[@]}"
 exit 0

@@ -147,3 +147,27 @@ def test_prediction_lookup_reads_the_newest_table():
         if n.endswith("_final.jsonl"):
             base = n.replace("_final", "")
             assert base not in names[:i], (base, n)
+
+
+def test_first_multigpu_report_grades_the_prediction(tmp_path):
+    """scripts/first_multigpu_report.py: a Tier A multi-GPU row is compared with the newest shipped prediction of
+    the same (strategy, dtype, N, seq); rows of other shapes are not graded."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    sys.path.insert(0, ROOT)
+    import bench
+    import first_multigpu_report as fmr
+    pred = bench.predicted_row("zero2-dp8", "bf16", 8, 2048)
+    assert pred is not None and pred["seq_len"] == 2048
+    assert bench.predicted_row("zero2-dp8", "bf16", 8, 64) is None
+    summ = tmp_path / "summary"
+    summ.mkdir()
+    hdr = ("strategy,world_size,rank,seq_len,tier,steps,per_device_batch,grad_accum,tokens_per_sec,"
+           "mean_step_time_sec,mean_loss,peak_vram_gb,h2d_gbps_per_gpu,scaling_efficiency_pct\n")
+    meas = pred["value"] * 0.9
+    (summ / "metrics.csv").write_text(hdr + "zero2,1,0,2048,A,100,1,4,280000,0.0073,5.0,9.5,1e-3,100.0\n"
+                                      f"zero2,8,0,2048,A,100,1,4,{meas},0.0080,5.0,3.9,1e-3,80.0\n"
+                                      "zero2,2,0,64,tiny,100,1,4,5000,0.02,5.0,0.1,1e-3,50.0\n")
+    out = fmr.write_report(str(tmp_path), str(summ / "first_multigpu_report.md"))
+    rep = open(out).read()
+    assert "-10.0 %" in rep and "| zero2 | 2 | 64 | tiny |" in rep
+    assert "Prediction error over 1 rows" in rep

@@ -161,16 +161,3 @@ def test_emulated_ddp_numerics_track_world1(comm, monkeypatch):
     assert w1[0] == e8[0]                                     # same init, same first batch
     for a, b in zip(w1, e8):
         assert abs(a - b) < 3e-3 * a, (w1, e8)
-
-
-@pytest.mark.gpu
-def test_ddp_early_update_matches_tail_update(monkeypatch):
-    """DDP at world > 1 runs each bucket's AdamW on a side stream as soon as its all-reduce lands
-    (DLTB_DDP_EARLY_OPT, parallel/replicated.py); the per-element update is the same as the tail
-    update's, so the loss curves must match exactly."""
-    monkeypatch.setenv("DLTB_COMM", "emulate:8")
-    monkeypatch.setenv("DLTB_DDP_EARLY_OPT", "0")
-    tail = _train_losses("compute")
-    monkeypatch.setenv("DLTB_DDP_EARLY_OPT", "1")
-    early = _train_losses("compute")
-    assert tail == early, (tail, early)

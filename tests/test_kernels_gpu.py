@@ -266,71 +266,6 @@ def test_gemm(tn, M, N, K, cfg, splits, pf, gm, stages):
     close(acc, ref32 + prev.float(), 0.1, 2e-2, "gemm accumulate")
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, -1])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (512, 768, 256), (2048, 1024, 1024)])
-@pytest.mark.parametrize("gm", [1, 4])
-def test_gemm_nt(cfg, M, N, K, gm):
-    """Own NT GEMM (csrc/gemm_nt.hip: loader / consumer waves, LDS-DMA or register-staged ring) vs
-    fp32 torch: bias, accumulate, a row-strided A view, and the one-workgroup-per-CU default pick."""
-    C_ = ext()
-    if not C_.gemm_nt_supported(M, N, K, cfg):
-        pytest.skip("tile config does not divide this shape")
-    a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
-    a = a_full[:, 32:K + 32]
-    ref32 = a.float() @ b.float().t()
-    bias = rnd(N)
-    out = C_.gemm_nt(a, b, None, bias, False, cfg, gm)
-    close(out, ref32 + bias.float(), 0.05, 2e-2, "gemm_nt + bias")
-    prev = rnd(M, N)
-    acc = prev.clone()
-    C_.gemm_nt(a, b, acc, None, True, cfg, gm)
-    close(acc, ref32 + prev.float(), 0.05, 2e-2, "gemm_nt accumulate")
-
-
-@pytest.mark.parametrize("cfg", [7, 8, 9])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (2048, 1024, 4096), (512, 384, 1536)])
-def test_gemm_nt_splitk(cfg, M, N, K):
-    """Split-K NT GEMM: two fp32 planes (bias in plane 0) whose sum is the fp32 product."""
-    C_ = ext()
-    if not C_.gemm_nt_supported(M, N, K, cfg):
-        pytest.skip("tile config does not divide this shape")
-    a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
-    a = a_full[:, 32:K + 32]
-    bias = rnd(N)
-    ref32 = a.float() @ b.float().t()
-    planes = C_.gemm_nt(a, b, None, bias, False, cfg, 4)
-    assert planes.dtype == torch.float32 and tuple(planes.shape) == (2, M, N)
-    close(planes.sum(0), ref32 + bias.float(), 2e-3, 1e-3, "gemm_nt split-K planes")
-    ref_lo = a[:, :K // 2].float() @ b[:, :K // 2].float().t()
-    close(planes[0], ref_lo + bias.float(), 2e-3, 1e-3, "gemm_nt split-K plane 0 = first half of K + bias")
-
-
-@pytest.mark.parametrize("M,N,K", [(256, 256, 512), (2048, 1024, 4096), (2048, 1024, 3072), (512, 384, 1536)])
-def test_gemm_nt_pair_fixup(M, N, K):
-    """Split-K NT GEMM with the pair fixup (cfg 10): bf16 output + bias, the two K halves summed in
-    fp32 by whichever wave of a pair finishes second; the pairs' counters are left zero, so the same
-    sync buffer serves launch after launch (3 launches here, and a fresh-buffer launch)."""
-    C_ = ext()
-    cfg = 10
-    if not C_.gemm_nt_supported(M, N, K, cfg):
-        pytest.skip("cfg 10 is A/B-only (DLTB_NT_FIXUP_AB=1) or does not divide this shape")
-    a_full, b = rnd(M, K + 64), rnd(N, K, scale=0.1)
-    a = a_full[:, 32:K + 32]
-    bias = rnd(N)
-    ref32 = a.float() @ b.float().t() + bias.float()
-    nsync = C_.gemm_nt_fixup_ints(cfg, M, N)
-    assert nsync == 8 * (M // 128) * (N // 128)
-    ws = torch.empty(M * N, device="cuda", dtype=torch.float32)
-    sync = torch.zeros(nsync, device="cuda", dtype=torch.int32)
-    for it in range(3):
-        out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
-        C_.gemm_nt(a, b, out, bias, False, cfg, 4, ws, sync)
-        assert bool(torch.isfinite(out).all()), "unwritten output elements"
-        close(out, ref32, 0.05, 2e-2, f"gemm_nt pair fixup (launch {it})")
-        assert int(sync.abs().sum()) == 0, "pair counters not cleared"
-    close(C_.gemm_nt(a, b, None, bias, False, cfg, 1), ref32, 0.05, 2e-2, "gemm_nt pair fixup (own buffers)")
-
-
 def test_swiglu_rope():
     C = ext()
     gu = rnd(256, 2 * 512)
@@ -545,7 +480,7 @@ def test_adamw_mixed_alignment_segments():
 
 
 def test_adamw_grid_cap_bitwise():
-    """A capped grid (DDP's side-stream early update, DLTB_DDP_EARLY_GRID) walks the block table
+    """A capped grid (launch_segment(grid_cap=...): an update trickled beside other kernels) walks the block table
     block-strided: bitwise the one-block-per-row launch."""
     C = ext()
     n = 300_000
@@ -636,35 +571,3 @@ def test_attn_mask_words_match_reference():
     want = rng.keep_mask(s, rows, cols, p).view(B * H, T, T)
     assert torch.equal(got, want)
 
-
-@pytest.mark.parametrize("N,d", [(512, 1024), (256, 768)])
-def test_norms_read_splitk_planes(N, d):
-    """The norm kernels' split-K inputs: a residual r (forward, with its dropout) or an upstream
-    gradient dy (fused backward) given as two fp32 planes [2, N, d] give what the same kernels give
-    for the planes' sum (rounded to bf16 there, so within bf16 tolerance)."""
-    from dltb.ops import functional as F_
-    C = ext()
-    x, w, b = rnd(N, d), rnd(d, scale=0.5) + 1, rnd(d, scale=0.1)
-    planes = torch.randn(2, N, d, device=DEV)
-    flat = planes.sum(0).to(torch.bfloat16)
-    sd = seed_obj(5)
-    s_p, y_p, mean_p, rstd_p = C.norm_fwd(x, planes, w, b, 1e-5, False, 0.1, sd.device_tensor, 9)
-    s_f, y_f, mean_f, rstd_f = C.norm_fwd(x, flat, w, b, 1e-5, False, 0.1, sd.device_tensor, 9)
-    close(s_p, s_f, 2e-2, 2e-2, "residual stream from planes")
-    close(y_p, y_f, 3e-2, 3e-2, "LN output from planes")
-    # fused backward: dy as planes vs dy as their bf16 sum
-    s_, dres = rnd(N, d), rnd(N, d)
-    mean = torch.randn(N, device=DEV) * 0.1
-    rstd = torch.rand(N, device=DEV) + 0.5
-    outs = []
-    for dy in (planes, flat):
-        gw = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
-        gb = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
-        bs = torch.zeros(d, device=DEV, dtype=torch.bfloat16)
-        red = F_.GradReducer()
-        dx = F_.norm_bwd(dy, s_, w, mean, rstd, dres, gw, gb, False, False, red=red, bias=("dx", bs, False))
-        red.flush()
-        outs.append((dx, gw, gb, bs))
-    for a, b_, what in zip(outs[0], outs[1], ("dx", "dgamma", "dbeta", "dx column sum")):
-        assert bool(torch.isfinite(a.float()).all()), what
-        close(a, b_, 5e-2 if what == "dx" else 0.5, 3e-2, f"{what} from planes")

@@ -10,6 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _suite(tmp_path, extra, strats="ddp zero2", m7b="0", **more):
+    more.setdefault("TRANSPORT_AB", "0")       # the full sequence runs in test_suite_ddp_zero2_world_1_and_2
+    more.setdefault("RCCL_CHECK", "0")
     env = dict(os.environ, STEPS="6", SEQ="64", TIER="tiny", WS_LIST="1 2", STRATS=strats, FORCE_NPROC="2",
                HARNESS_EXTRA=f"--device cpu --warmup-steps 2 --log-every 0 {extra}", TIMEOUT="300",
                OMP_NUM_THREADS="1", M7B=m7b, M7B_TIER="mtiny", M7B_SEQ="64", M7B_STEPS="6", M7B_WS="1 2", **more)
@@ -20,7 +22,19 @@ def _suite(tmp_path, extra, strats="ddp zero2", m7b="0", **more):
 
 
 def test_suite_ddp_zero2_world_1_and_2(tmp_path):
-    _suite(tmp_path, "")
+    """The whole first-multi-GPU sequence, rehearsed on gloo: equivalence check, collective
+    sweep, transport A/B on the flagship, the strategy matrix, CSV / plots / report, the multi-GPU summary page."""
+    _suite(tmp_path, "", TRANSPORT_AB="1", RCCL_CHECK="1")
+    eq = json.load(open(tmp_path / "summary" / "rccl_equivalence.json"))
+    assert eq["pass"] and eq["device"] == "cpu" and set(eq["world_sizes"]) == {"2"}
+    tab = [json.loads(ln) for ln in open(tmp_path / "summary" / "transport_ab.jsonl")]
+    assert [t["transport"] for t in tab] == ["default", "NCCL_MIN_NCHANNELS=16", "NCCL_MIN_NCHANNELS=32",
+                                             "DLTB_COMM_HIGH_PRIORITY=0"]
+    assert all(t["n_gpus"] == 2 and t["value"] > 0 for t in tab)
+    rep = (tmp_path / "summary" / "first_multigpu_report.md").read_text()
+    for sec in ("## Measured curve", "## Fabric: alpha-beta fit", "## RCCL transport A/B", "## RCCL equivalence"):
+        assert sec in rep, sec
+    assert "| zero2 | 2 |" in rep and "reduce_scatter" in rep and "Verdict: **pass**" in rep
     df = pd.read_csv(tmp_path / "summary" / "metrics.csv")
     assert sorted(zip(df.strategy, df.world_size)) == [("ddp", 1), ("ddp", 2), ("zero2", 1), ("zero2", 2)]
     assert (df.loc[df.world_size == 1, "scaling_efficiency_pct"] == 100.0).all()

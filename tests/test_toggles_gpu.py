@@ -7,10 +7,8 @@ dropout-backward paths were measured neutral or slower and deleted):
 * DLTB_DEFER_OPT                  -- world > 1 only: tests/test_multirank_gpu.py runs ZeRO-1/2 both ways
 * DLTB_DKDV_GSPLIT                -- causal GQA dK/dV head split, forced off vs auto, below
 * DLTB_COMM_HIGH_PRIORITY         -- an RCCL stream priority (no effect on results; needs >1 GPU)
-* DLTB_SPLITK_PLANES              -- split-K fp32 planes read by the norms (round 4, off: slower in the step);
-                                     tests/test_model_gpu.py::test_splitk_planes_step_matches_hipblaslt_step
-* DLTB_FWD_PP / DLTB_NT_FIXMODE   -- build-time / A-B-only kernel variants (attention ping-pong, split-K pair
-                                     fixup ablation); their numerics run in tests/test_kernels_gpu.py on A/B builds
+(The split-K fp32-plane GEMM path, the attention ping-pong forward and the side-stream dW / early DDP update
+were measured slower and deleted in round 6; the toggle table is docs/ARCHITECTURE.md "Runtime switches".)
 """
 import os
 import subprocess
