@@ -1,0 +1,423 @@
+// bf16 "TN" GEMM for weight gradients (gfx950, CDNA4):
+//
+//   C[b][M][N] (+)= sum_k A[b][k][m] . B[b][k][n]          fp32 accumulate, bf16 out
+//
+// A weight gradient dW = dY^T X has the token (reduction) index as the OUTER dimension of both operands
+// (dY [T][out], X [T][in], both row-major), so neither operand is K-contiguous.  hipBLASLt runs that layout
+// 25-45 % slower than the K-contiguous one (profiles/gemm_layouts_r2.txt: 1.03-1.04 against 1.48-1.52
+// PFLOP/s on the same shapes; the TinyGPT-A window-wide batched dW at 1.07-1.17).  Here the operands
+// are staged as they lie -- 64 token rows x 256 feature columns per operand and k-step, filled by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB = two 512-byte rows per wave-instruction) -- and the MFMA fragments
+// are read TRANSPOSED out of LDS with ds_read_b64_tr_b16, which hands each lane 4 consecutive tokens of
+// one feature column: the layout costs no extra pass and no extra LDS traffic.
+//
+// Tile 256 (m) x 256 (n) x 64 (k), 512 threads = 8 waves as 2 (m) x 4 (n), each wave 128 x 64 outputs on
+// v_mfma_f32_16x16x32_bf16 (8 x 4 accumulators).  MFMA operands swapped (the X fragment is the MFMA's A
+// operand), so a lane holds 4 consecutive n of one m: 8-byte epilogue stores.  Two 64 KiB stage buffers:
+// the DMA of stage kt + 2 is issued right after every wave finished reading stage kt, and runs under the
+// MFMAs of stage kt + 1 (counted vmcnt, raw s_barrier: the loads stay in flight across the barrier).
+//
+// LDS image of one operand and stage: [64 k][256 cols] bf16, 512-byte rows; the 32-byte segment s (16
+// columns) of row k is stored at segment s ^ h(k), h(k) = (k & 3) | ((k >> 3) & 1) << 2.  A transposed
+// read of one 32-lane half touches 8 rows (k = 8g + q + 4hh over g = 0, 1 and q = 0..3) of one column
+// segment: h maps them to the 8 distinct 32-byte bank segments of a 256-byte bank row (conflict-free).
+// The swizzle is applied on the DMA's SOURCE address (the LDS side of an LDS-DMA is lane-linear).
+#include "common.h"
+#include "launchers.h"
+#include "mfma_tiles.h"
+
+namespace {
+
+constexpr int kTM = 256, kTN = 256, kTK = 64;
+constexpr int kRowB = 512;                    // bytes per k-row of an operand image (256 bf16)
+constexpr int kImg = kTK * kRowB;             // 32 KiB: one operand, one stage
+constexpr int kStage = 2 * kImg;              // A image, then B image
+constexpr int kGlds = kImg / 1024 / 8;        // LDS-DMA wave-instructions per wave, operand and stage (4)
+
+struct TnArgs {
+  const bf16_t* a;
+  const bf16_t* b;
+  bf16_t* c;
+  long lda, ldb, ldc;                         // row strides (elements)
+  long sa, sb, sc;                            // batch strides (elements)
+  int M, N, K, batch;
+  int accumulate;
+};
+
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+DLTB_DEV f4 mfma16(bfx8 a, bfx8 b, f4 c) {
+#if DLTB_F16
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
+
+DLTB_DEV int tn_h(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+// workgroup barrier that is also a compiler barrier for LDS accesses (no read of a stage may be moved
+// across the barrier that orders it against the DMA refilling that stage)
+DLTB_DEV void tn_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// one operand fragment (16 columns x 32 k) by two transposed reads at lane byte offset `off` of a stage
+// image: element j of lane l = image[k0 + 8 (l >> 4) + j][column c0 + (l & 15)]
+template <int OFF>
+DLTB_DEV bfx8 tn_frag(uint32_t base, uint32_t off) {
+  return tr_frag_at<OFF>(base + off, base + off + 4 * kRowB);
+}
+
+// V = 1: two barriers per k-step (reads of stage kt done -> refill; stage kt + 1 landed), the fragments of a
+//        k-substep read in one burst before its 32 MFMAs.
+// V = 2: one barrier per k-step (the refill of stage kt + 2 is issued right after the barrier that
+//        publishes stage kt + 1, which is also the barrier after every wave's last read of stage kt), and the
+//        second k-substep's fragments are read in the shadow of the first's MFMAs: after the 4 MFMAs of m-tile
+//        i its A fragment's registers take the next substep's A fragment i (the B fragments of substep 1 in a
+//        second register set, read first), the issue order pinned with scheduling fences.
+template <int V>
+__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- tile walk: each XCD (workgroups b, b + 8, ... under round-robin dispatch: speed only) takes a
+  // contiguous run of (batch, m-tile, n-tile) so the panels its tiles share stay in its L2
+  const int tm = g.M / kTM, tn = g.N / kTN, per = tm * tn, tiles = per * g.batch;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  const int bt = idx / per, rem = idx - bt * per;
+  const int mb = rem / tn, nb = rem - mb * tn;
+  const int m0 = mb * kTM, n0 = nb * kTN;
+  const int nk = g.K / kTK;
+  DLTB_DCHECK(bt < g.batch && m0 + kTM <= g.M && n0 + kTN <= g.N && nk * kTK == g.K && nk >= 2);
+
+  const bf16_t* abase = g.a + (long)bt * g.sa + m0;
+  const bf16_t* bbase = g.b + (long)bt * g.sb + n0;
+  // LDS-DMA source offsets (loop-invariant): instruction i of this wave fills image bytes
+  // [(wave * kGlds + i) KiB, + 1 KiB) = rows 2 (wave * kGlds + i) + lane / 32, physical 16-byte chunk lane % 32
+  uint32_t oa[kGlds], ob[kGlds];
+#pragma unroll
+  for (int i = 0; i < kGlds; ++i) {
+    const int row = 2 * (wave * kGlds + i) + (lane >> 5), c = lane & 31;
+    const int col = (((c >> 1) ^ tn_h(row)) << 4) + (c & 1) * 8;          // logical column of this chunk
+    oa[i] = (uint32_t)((row * g.lda + col) * 2);
+    ob[i] = (uint32_t)((row * g.ldb + col) * 2);
+  }
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  auto issue = [&](int kt, int buf) {
+    const bf16_t* pa = abase + (long)kt * kTK * g.lda;
+    const bf16_t* pb = bbase + (long)kt * kTK * g.ldb;
+    char* img = smem + buf * kStage;
+#pragma unroll
+    for (int i = 0; i < kGlds; ++i) glds16_sv(pa, oa[i], img + (wave * kGlds + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < kGlds; ++i) glds16_sv(pb, ob[i], img + kImg + (wave * kGlds + i) * 1024);
+  };
+
+  // ---- fragment read offsets: lane l = 16 g + 4 q + p reads row 8 g + q (+ 4 for the second half) and
+  // columns c0 + 4 p of a fragment; h(row) = q | (g & 1) << 2 for every k-substep and half
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int hq = fq | ((fg & 1) << 2);
+  const uint32_t rowoff = (uint32_t)((8 * fg + fq) * kRowB + 8 * fp);
+  uint32_t offm[8], offn[4];        // per m-tile (image A) / n-tile (image B) lane offsets
+#pragma unroll
+  for (int i = 0; i < 8; ++i) offm[i] = rowoff + ((((wm * 128 + 16 * i) >> 4) ^ hq) << 5);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) offn[j] = kImg + rowoff + ((((wn * 64 + 16 * j) >> 4) ^ hq) << 5);
+
+  f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint32_t base = lds0 + buf * kStage;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bfx8 fa[8], fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = ks ? tn_frag<32 * kRowB>(base, offn[j]) : tn_frag<0>(base, offn[j]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = ks ? tn_frag<32 * kRowB>(base, offm[i]) : tn_frag<0>(base, offm[i]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+    }
+  };
+  // V = 2: substep 0 from registers read before the call (fa / fb), substep 1 read in its shadow
+  auto compute_pipe = [&](int buf, bfx8 (&fa)[8], bfx8 (&fb)[4]) {
+    const uint32_t base = lds0 + buf * kStage;
+    bfx8 fb1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb1[j] = tn_frag<32 * kRowB>(base, offn[j]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
+      fa[i] = tn_frag<32 * kRowB>(base, offm[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb1[j], fa[i], acc[i][j]);
+  };
+  auto read0 = [&](int buf, bfx8 (&fa)[8], bfx8 (&fb)[4]) {
+    const uint32_t base = lds0 + buf * kStage;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = tn_frag<0>(base, offn[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = tn_frag<0>(base, offm[i]);
+  };
+
+  issue(0, 0);
+  issue(1, 1);
+  wait_vm<2 * kGlds>();                     // this wave's stage-0 DMAs landed (stage 1's may remain)
+  tn_barrier();                             // ... and every wave's
+  if constexpr (V == 1) {
+    // ---- stage kt in buffer kt & 1; the DMA of stage kt + 2 refills it once every wave is done with it
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      compute(buf);
+      if (kt + 2 < nk) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        tn_barrier();                       // every wave's reads of `buf` done
+        __builtin_amdgcn_sched_barrier(0);
+        issue(kt + 2, buf);
+        wait_vm<2 * kGlds>();               // stage kt + 1 landed (stage kt + 2 in flight)
+      } else {
+        wait_vm<0>();
+      }
+      tn_barrier();                         // stage kt + 1 visible to every wave
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    // ---- top of step kt: stage kt landed and published, stage kt + 1 in flight
+    bfx8 fa[8], fb[4];
+    read0(0, fa, fb);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      compute_pipe(buf, fa, fb);
+      wait_vm<0>();                          // this wave's DMAs of stage kt + 1 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      tn_barrier();                          // everyone's: stage kt + 1 published, stage kt's reads done
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < nk) read0(buf ^ 1, fa, fb);
+      if (kt + 2 < nk) issue(kt + 2, buf);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- epilogue: lane (16 g' + r) holds C[m0 + 128 wm + 16 i + r][n0 + 64 wn + 16 j + 4 g' .. + 3]
+  const int er = lane & 15, eg = lane >> 4;
+  bf16_t* cbase = g.c + (long)bt * g.sc + (long)(m0 + wm * 128 + er) * g.ldc + n0 + wn * 64 + 4 * eg;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16_t* dst = cbase + (long)(16 * i) * g.ldc + 16 * j;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.accumulate) {
+        const uint2 old = *reinterpret_cast<const uint2*>(dst);
+        v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+      }
+      uint2 o;
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(dst) = o;
+    }
+  }
+}
+
+// V = 3: 32-deep k-steps in a ring of four 32 KiB stages (128 KiB), two fragment register sets.  Step kt
+// computes stage kt from registers (read during step kt - 1) while reading stage kt + 1's fragments into
+// the other set, and refills the buffer stage kt's fragments came from with stage kt + 4 (every wave read
+// it before the barrier that ended step kt - 1); one barrier per step publishes stage kt + 2 (its DMA was
+// issued two steps earlier; stages kt + 3 / kt + 4 stay in flight across it).  No fragment read is exposed
+// at a step boundary, unlike V = 2, whose first substep reads follow the barrier.
+constexpr int kTK3 = 32;
+constexpr int kImg3 = kTK3 * kRowB;           // 16 KiB
+constexpr int kStage3 = 2 * kImg3;            // 32 KiB
+constexpr int kRing3 = 4;
+constexpr int kGlds3 = kImg3 / 1024 / 8;      // 2 per wave, operand and stage
+
+// SPREAD: the refill's LDS-DMA instructions (each holds its wave ~60-100 cycles at issue) are spread over
+// the step's MFMA groups instead of issued back to back at its start; PRIO: s_setprio 1 around each MFMA group.
+template <bool SPREAD, bool PRIO>
+__global__ __launch_bounds__(512, 1) void gemm_tn3_kernel(TnArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tm = g.M / kTM, tn = g.N / kTN, per = tm * tn, tiles = per * g.batch;
+  const int L = blockIdx.x;
+  int idx = L;
+  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  const int bt = idx / per, rem = idx - bt * per;
+  const int mb = rem / tn, nb = rem - mb * tn;
+  const int m0 = mb * kTM, n0 = nb * kTN;
+  const int nk = g.K / kTK3;
+  DLTB_DCHECK(bt < g.batch && m0 + kTM <= g.M && n0 + kTN <= g.N && nk * kTK3 == g.K && nk >= 4 && nk % 2 == 0);
+
+  const bf16_t* abase = g.a + (long)bt * g.sa + m0;
+  const bf16_t* bbase = g.b + (long)bt * g.sb + n0;
+  uint32_t oa[kGlds3], ob[kGlds3];
+#pragma unroll
+  for (int i = 0; i < kGlds3; ++i) {
+    const int row = 2 * (wave * kGlds3 + i) + (lane >> 5), c = lane & 31;
+    const int col = (((c >> 1) ^ tn_h(row)) << 4) + (c & 1) * 8;
+    oa[i] = (uint32_t)((row * g.lda + col) * 2);
+    ob[i] = (uint32_t)((row * g.ldb + col) * 2);
+  }
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  // DMA instruction q (0 .. 2 kGlds3 - 1) of stage kt: the A image's kGlds3, then the B image's
+  auto issue1 = [&](int kt, int q) {
+    char* img = smem + (kt & (kRing3 - 1)) * kStage3;
+    if (q < kGlds3) glds16_sv(abase + (long)kt * kTK3 * g.lda, oa[q], img + (wave * kGlds3 + q) * 1024);
+    else glds16_sv(bbase + (long)kt * kTK3 * g.ldb, ob[q - kGlds3], img + kImg3 + (wave * kGlds3 + q - kGlds3) * 1024);
+  };
+  auto issue = [&](int kt) {
+#pragma unroll
+    for (int q = 0; q < 2 * kGlds3; ++q) issue1(kt, q);
+  };
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int hq = fq | ((fg & 1) << 2);
+  const uint32_t rowoff = (uint32_t)((8 * fg + fq) * kRowB + 8 * fp);
+  uint32_t offm[8], offn[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) offm[i] = rowoff + ((((wm * 128 + 16 * i) >> 4) ^ hq) << 5);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) offn[j] = kImg3 + rowoff + ((((wn * 64 + 16 * j) >> 4) ^ hq) << 5);
+
+  f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  auto read_all = [&](int kt, bfx8 (&fa)[8], bfx8 (&fb)[4]) {
+    const uint32_t base = lds0 + (kt & (kRing3 - 1)) * kStage3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = tn_frag<0>(base, offn[j]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = tn_frag<0>(base, offm[i]);
+  };
+  // one step: MFMAs of stage kt (ca / cb) || fragments of stage kt + 1 (na / nb); refill; publish kt + 2
+  auto step = [&](int kt, bfx8 (&ca)[8], bfx8 (&cb)[4], bfx8 (&na)[8], bfx8 (&nb)[4]) {
+    const bool refill = kt + 4 < nk;              // into stage kt's buffer (read during step kt - 1)
+    if (!SPREAD && refill) issue(kt + 4);
+    const bool nxt = kt + 1 < nk;
+    const uint32_t nbase = lds0 + ((kt + 1) & (kRing3 - 1)) * kStage3;
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (nxt) {
+        if (i < 4) nb[i] = tn_frag<0>(nbase, offn[i]);
+        na[i] = tn_frag<0>(nbase, offm[i]);
+      }
+      if (SPREAD && refill && (i & 1) == 0) issue1(kt + 4, i >> 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // publish stage kt + 2: this wave's DMAs of it landed (later stages may stay in flight), then the barrier
+    const int later = min(nk - 1, kt + 4) - (kt + 2);     // stages issued after kt + 2
+    if (later >= 2) wait_vm<4 * kGlds3>();
+    else if (later == 1) wait_vm<2 * kGlds3>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tn_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: stages 0..3 in flight; 0 and 1 published; stage 0's fragments in set A
+#pragma unroll
+  for (int s = 0; s < kRing3; ++s) issue(s);
+  wait_vm<4 * kGlds3>();                       // stages 0, 1 landed (2, 3 in flight)
+  tn_barrier();
+  bfx8 fa0[8], fb0[4], fa1[8], fb1[4];
+  read_all(0, fa0, fb0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  tn_barrier();                                // every wave read stage 0: step 0 may refill its buffer
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, fa0, fb0, fa1, fb1);
+    step(kt + 1, fa1, fb1, fa0, fb0);
+  }
+  wait_vm<0>();
+
+  const int er = lane & 15, eg = lane >> 4;
+  bf16_t* cbase = g.c + (long)bt * g.sc + (long)(m0 + wm * 128 + er) * g.ldc + n0 + wn * 64 + 4 * eg;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16_t* dst = cbase + (long)(16 * i) * g.ldc + 16 * j;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (g.accumulate) {
+        const uint2 old = *reinterpret_cast<const uint2*>(dst);
+        v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
+      }
+      uint2 o;
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<uint2*>(dst) = o;
+    }
+  }
+}
+
+}  // namespace
+
+bool dltb_gemm_tn_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && K > 0 && M % kTM == 0 && N % kTN == 0 && K % kTK == 0 && K / kTK >= 2;
+}
+
+int dltb_gemm_tn(const void* a, const void* b, void* c, long lda, long ldb, long ldc, long sa, long sb, long sc,
+                 int M, int N, int K, int batch, int accumulate, hipStream_t st, int variant) {
+  if (!dltb_gemm_tn_supported(M, N, K) || batch < 1) return -1;
+  TnArgs g{};
+  g.a = (const bf16_t*)a;
+  g.b = (const bf16_t*)b;
+  g.c = (bf16_t*)c;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.ldc = ldc;
+  g.sa = sa;
+  g.sb = sb;
+  g.sc = sc;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.batch = batch;
+  g.accumulate = accumulate;
+  constexpr int smem = 2 * kStage;
+  static_assert(kRing3 * kStage3 == smem, "V3 ring = the two V1/V2 stages");
+  int v = variant >= 1 && variant <= 5 ? variant : 3;
+  if (v >= 3 && (K % (2 * kTK3) != 0 || K / kTK3 < 4)) v = 2;   // the ring kernels step in pairs, fill 4 stages
+  static bool attr[5] = {false, false, false, false, false};
+  const void* fns[5] = {(const void*)gemm_tn_kernel<1>, (const void*)gemm_tn_kernel<2>,
+                        (const void*)gemm_tn3_kernel<true, false>, (const void*)gemm_tn3_kernel<true, true>,
+                        (const void*)gemm_tn3_kernel<false, false>};
+  if (!attr[v - 1]) {
+    (void)hipFuncSetAttribute(fns[v - 1], hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr[v - 1] = true;
+  }
+  const dim3 grid((unsigned)((long)(M / kTM) * (N / kTN) * batch));
+  switch (v) {
+    case 1: hipLaunchKernelGGL(gemm_tn_kernel<1>, grid, dim3(512), smem, st, g); break;
+    case 2: hipLaunchKernelGGL(gemm_tn_kernel<2>, grid, dim3(512), smem, st, g); break;
+    case 3: hipLaunchKernelGGL((gemm_tn3_kernel<true, false>), grid, dim3(512), smem, st, g); break;
+    case 4: hipLaunchKernelGGL((gemm_tn3_kernel<true, true>), grid, dim3(512), smem, st, g); break;
+    default: hipLaunchKernelGGL((gemm_tn3_kernel<false, false>), grid, dim3(512), smem, st, g); break;
+  }
+  return 0;
+}

@@ -70,7 +70,10 @@ class ShardedEngine(Engine):
             return [units]
         if self.cfg.wrap == "unit":
             return [[u] for u in units]
-        # "block": transformer blocks own a group each; embedding + head form the root group
+        # "block": transformer blocks own a group each; embedding + head form the root group.  (Splitting the
+        # tied head into a group of its own, reduced right after the head's backward, measured no better at
+        # emulated N = 2 / 8: the exposed tail is the per-block re-gather + reduce-scatter queue of the
+        # backward, not the table: profiles/fsdp_split_root_ab_r6.txt.)
         root = [units[0], units[-1]]
         return [root] + [[u] for u in units[1:-1]]
 

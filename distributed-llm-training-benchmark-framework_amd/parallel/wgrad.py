@@ -58,6 +58,7 @@ class WgradQueue:
         self._items: Dict[int, list] = defaultdict(list)     # id(unit) -> [(i, dy, x, dw, acc)]
         self.batched_calls = 0
         self.single_calls = 0
+        self.tn_calls = 0            # batched products that ran on the own token-major kernel (gemm_tn)
 
     def add(self, unit, i, dy, x, dw, accumulate):
         self._items[id(unit)].append((i, dy, x, dw, bool(accumulate)))
@@ -93,7 +94,9 @@ class WgradQueue:
                     # BLAS TN batched: hipBLASLt's heuristic solution for it faulted the GPU
                     # (profiles/dw_layout_probe_fault_r4.txt); the layer buffers are row-major
                     raise RuntimeError("batched dW with a column-major X operand (BLAS TN) is refused")
-                if _blt.mm(DY.transpose(1, 2), X, DW, acc):
+                if F_.own_wgrad(DY, X, DW, acc):
+                    self.tn_calls += 1
+                elif _blt.mm(DY.transpose(1, 2), X, DW, acc):
                     pass
                 elif acc:
                     DW.baddbmm_(DY.transpose(1, 2), X)
