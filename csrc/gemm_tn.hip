@@ -11,13 +11,12 @@
 // are read TRANSPOSED out of LDS with ds_read_b64_tr_b16, which hands each lane 4 consecutive tokens of
 // one feature column: the layout costs no extra pass and no extra LDS traffic.
 //
-// Tile 256 (m) x 256 (n) x 64 (k), 512 threads = 8 waves as 2 (m) x 4 (n), each wave 128 x 64 outputs on
+// Tile 256 (m) x 256 (n), 512 threads = 8 waves as 2 (m) x 4 (n), each wave 128 x 64 outputs on
 // v_mfma_f32_16x16x32_bf16 (8 x 4 accumulators).  MFMA operands swapped (the X fragment is the MFMA's A
-// operand), so a lane holds 4 consecutive n of one m: 8-byte epilogue stores.  Two 64 KiB stage buffers:
-// the DMA of stage kt + 2 is issued right after every wave finished reading stage kt, and runs under the
-// MFMAs of stage kt + 1 (counted vmcnt, raw s_barrier: the loads stay in flight across the barrier).
+// operand), so a lane holds 4 consecutive n of one m: 8-byte epilogue stores.  The DMA of a stage runs two
+// to three k-steps ahead (counted vmcnt, raw s_barrier: the loads stay in flight across the barrier).
 //
-// LDS image of one operand and stage: [64 k][256 cols] bf16, 512-byte rows; the 32-byte segment s (16
+// LDS image of one operand and stage: [32 k][256 cols] bf16, 512-byte rows; the 32-byte segment s (16
 // columns) of row k is stored at segment s ^ h(k), h(k) = (k & 3) | ((k >> 3) & 1) << 2.  A transposed
 // read of one 32-lane half touches 8 rows (k = 8g + q + 4hh over g = 0, 1 and q = 0..3) of one column
 // segment: h maps them to the 8 distinct 32-byte bank segments of a 256-byte bank row (conflict-free).
@@ -28,11 +27,8 @@
 
 namespace {
 
-constexpr int kTM = 256, kTN = 256, kTK = 64;
+constexpr int kTM = 256, kTN = 256;
 constexpr int kRowB = 512;                    // bytes per k-row of an operand image (256 bf16)
-constexpr int kImg = kTK * kRowB;             // 32 KiB: one operand, one stage
-constexpr int kStage = 2 * kImg;              // A image, then B image
-constexpr int kGlds = kImg / 1024 / 8;        // LDS-DMA wave-instructions per wave, operand and stage (4)
 
 struct TnArgs {
   const bf16_t* a;
@@ -67,190 +63,22 @@ DLTB_DEV bfx8 tn_frag(uint32_t base, uint32_t off) {
   return tr_frag_at<OFF>(base + off, base + off + 4 * kRowB);
 }
 
-// V = 1: two barriers per k-step (reads of stage kt done -> refill; stage kt + 1 landed), the fragments of a
-//        k-substep read in one burst before its 32 MFMAs.
-// V = 2: one barrier per k-step (the refill of stage kt + 2 is issued right after the barrier that
-//        publishes stage kt + 1, which is also the barrier after every wave's last read of stage kt), and the
-//        second k-substep's fragments are read in the shadow of the first's MFMAs: after the 4 MFMAs of m-tile
-//        i its A fragment's registers take the next substep's A fragment i (the B fragments of substep 1 in a
-//        second register set, read first), the issue order pinned with scheduling fences.
-template <int V>
-__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-
-  // ---- tile walk: each XCD (workgroups b, b + 8, ... under round-robin dispatch: speed only) takes a
-  // contiguous run of (batch, m-tile, n-tile) so the panels its tiles share stay in its L2
-  const int tm = g.M / kTM, tn = g.N / kTN, per = tm * tn, tiles = per * g.batch;
-  const int L = blockIdx.x;
-  int idx = L;
-  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
-  const int bt = idx / per, rem = idx - bt * per;
-  const int mb = rem / tn, nb = rem - mb * tn;
-  const int m0 = mb * kTM, n0 = nb * kTN;
-  const int nk = g.K / kTK;
-  DLTB_DCHECK(bt < g.batch && m0 + kTM <= g.M && n0 + kTN <= g.N && nk * kTK == g.K && nk >= 2);
-
-  const bf16_t* abase = g.a + (long)bt * g.sa + m0;
-  const bf16_t* bbase = g.b + (long)bt * g.sb + n0;
-  // LDS-DMA source offsets (loop-invariant): instruction i of this wave fills image bytes
-  // [(wave * kGlds + i) KiB, + 1 KiB) = rows 2 (wave * kGlds + i) + lane / 32, physical 16-byte chunk lane % 32
-  uint32_t oa[kGlds], ob[kGlds];
-#pragma unroll
-  for (int i = 0; i < kGlds; ++i) {
-    const int row = 2 * (wave * kGlds + i) + (lane >> 5), c = lane & 31;
-    const int col = (((c >> 1) ^ tn_h(row)) << 4) + (c & 1) * 8;          // logical column of this chunk
-    oa[i] = (uint32_t)((row * g.lda + col) * 2);
-    ob[i] = (uint32_t)((row * g.ldb + col) * 2);
-  }
-  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
-  auto issue = [&](int kt, int buf) {
-    const bf16_t* pa = abase + (long)kt * kTK * g.lda;
-    const bf16_t* pb = bbase + (long)kt * kTK * g.ldb;
-    char* img = smem + buf * kStage;
-#pragma unroll
-    for (int i = 0; i < kGlds; ++i) glds16_sv(pa, oa[i], img + (wave * kGlds + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < kGlds; ++i) glds16_sv(pb, ob[i], img + kImg + (wave * kGlds + i) * 1024);
-  };
-
-  // ---- fragment read offsets: lane l = 16 g + 4 q + p reads row 8 g + q (+ 4 for the second half) and
-  // columns c0 + 4 p of a fragment; h(row) = q | (g & 1) << 2 for every k-substep and half
-  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
-  const int hq = fq | ((fg & 1) << 2);
-  const uint32_t rowoff = (uint32_t)((8 * fg + fq) * kRowB + 8 * fp);
-  uint32_t offm[8], offn[4];        // per m-tile (image A) / n-tile (image B) lane offsets
-#pragma unroll
-  for (int i = 0; i < 8; ++i) offm[i] = rowoff + ((((wm * 128 + 16 * i) >> 4) ^ hq) << 5);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) offn[j] = kImg + rowoff + ((((wn * 64 + 16 * j) >> 4) ^ hq) << 5);
-
-  f4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint32_t base = lds0 + buf * kStage;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bfx8 fa[8], fb[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = ks ? tn_frag<32 * kRowB>(base, offn[j]) : tn_frag<0>(base, offn[j]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) fa[i] = ks ? tn_frag<32 * kRowB>(base, offm[i]) : tn_frag<0>(base, offm[i]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
-    }
-  };
-  // V = 2: substep 0 from registers read before the call (fa / fb), substep 1 read in its shadow
-  auto compute_pipe = [&](int buf, bfx8 (&fa)[8], bfx8 (&fb)[4]) {
-    const uint32_t base = lds0 + buf * kStage;
-    bfx8 fb1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb1[j] = tn_frag<32 * kRowB>(base, offn[j]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
-      __builtin_amdgcn_sched_barrier(0);
-      fa[i] = tn_frag<32 * kRowB>(base, offm[i]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb1[j], fa[i], acc[i][j]);
-  };
-  auto read0 = [&](int buf, bfx8 (&fa)[8], bfx8 (&fb)[4]) {
-    const uint32_t base = lds0 + buf * kStage;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = tn_frag<0>(base, offn[j]);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = tn_frag<0>(base, offm[i]);
-  };
-
-  issue(0, 0);
-  issue(1, 1);
-  wait_vm<2 * kGlds>();                     // this wave's stage-0 DMAs landed (stage 1's may remain)
-  tn_barrier();                             // ... and every wave's
-  if constexpr (V == 1) {
-    // ---- stage kt in buffer kt & 1; the DMA of stage kt + 2 refills it once every wave is done with it
-    for (int kt = 0; kt < nk; ++kt) {
-      const int buf = kt & 1;
-      compute(buf);
-      if (kt + 2 < nk) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        tn_barrier();                       // every wave's reads of `buf` done
-        __builtin_amdgcn_sched_barrier(0);
-        issue(kt + 2, buf);
-        wait_vm<2 * kGlds>();               // stage kt + 1 landed (stage kt + 2 in flight)
-      } else {
-        wait_vm<0>();
-      }
-      tn_barrier();                         // stage kt + 1 visible to every wave
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    // ---- top of step kt: stage kt landed and published, stage kt + 1 in flight
-    bfx8 fa[8], fb[4];
-    read0(0, fa, fb);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int buf = kt & 1;
-      compute_pipe(buf, fa, fb);
-      wait_vm<0>();                          // this wave's DMAs of stage kt + 1 landed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      tn_barrier();                          // everyone's: stage kt + 1 published, stage kt's reads done
-      __builtin_amdgcn_sched_barrier(0);
-      if (kt + 1 < nk) read0(buf ^ 1, fa, fb);
-      if (kt + 2 < nk) issue(kt + 2, buf);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-
-  // ---- epilogue: lane (16 g' + r) holds C[m0 + 128 wm + 16 i + r][n0 + 64 wn + 16 j + 4 g' .. + 3]
-  const int er = lane & 15, eg = lane >> 4;
-  bf16_t* cbase = g.c + (long)bt * g.sc + (long)(m0 + wm * 128 + er) * g.ldc + n0 + wn * 64 + 4 * eg;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bf16_t* dst = cbase + (long)(16 * i) * g.ldc + 16 * j;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (g.accumulate) {
-        const uint2 old = *reinterpret_cast<const uint2*>(dst);
-        v[0] += lo_bf(old.x); v[1] += hi_bf(old.x); v[2] += lo_bf(old.y); v[3] += hi_bf(old.y);
-      }
-      uint2 o;
-      o.x = pack_bf2(v[0], v[1]);
-      o.y = pack_bf2(v[2], v[3]);
-      *reinterpret_cast<uint2*>(dst) = o;
-    }
-  }
-}
-
-// V = 3: 32-deep k-steps in a ring of four 32 KiB stages (128 KiB), two fragment register sets.  Step kt
+// The main loop: 32-deep k-steps in a ring of four 32 KiB stages (128 KiB), two fragment register sets.  Step kt
 // computes stage kt from registers (read during step kt - 1) while reading stage kt + 1's fragments into
 // the other set, and refills the buffer stage kt's fragments came from with stage kt + 4 (every wave read
 // it before the barrier that ended step kt - 1); one barrier per step publishes stage kt + 2 (its DMA was
 // issued two steps earlier; stages kt + 3 / kt + 4 stay in flight across it).  No fragment read is exposed
-// at a step boundary, unlike V = 2, whose first substep reads follow the barrier.
+// at a step boundary.  (Measured against it on the dW shapes, profiles/gemm_tn_r6.txt: 64-deep k-steps in
+// two stage buffers with two barriers per step, 8-10 % slower; the same with one barrier and the second
+// substep's reads pipelined, 3-5 % slower; the refill's DMA spread over the MFMA groups and s_setprio
+// around them, within +-2 %.)
 constexpr int kTK3 = 32;
 constexpr int kImg3 = kTK3 * kRowB;           // 16 KiB
 constexpr int kStage3 = 2 * kImg3;            // 32 KiB
 constexpr int kRing3 = 4;
 constexpr int kGlds3 = kImg3 / 1024 / 8;      // 2 per wave, operand and stage
 
-// SPREAD: the refill's LDS-DMA instructions (each holds its wave ~60-100 cycles at issue) are spread over
-// the step's MFMA groups instead of issued back to back at its start; PRIO: s_setprio 1 around each MFMA group.
-template <bool SPREAD, bool PRIO>
-__global__ __launch_bounds__(512, 1) void gemm_tn3_kernel(TnArgs g) {
+__global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -276,15 +104,14 @@ __global__ __launch_bounds__(512, 1) void gemm_tn3_kernel(TnArgs g) {
     ob[i] = (uint32_t)((row * g.ldb + col) * 2);
   }
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
-  // DMA instruction q (0 .. 2 kGlds3 - 1) of stage kt: the A image's kGlds3, then the B image's
-  auto issue1 = [&](int kt, int q) {
-    char* img = smem + (kt & (kRing3 - 1)) * kStage3;
-    if (q < kGlds3) glds16_sv(abase + (long)kt * kTK3 * g.lda, oa[q], img + (wave * kGlds3 + q) * 1024);
-    else glds16_sv(bbase + (long)kt * kTK3 * g.ldb, ob[q - kGlds3], img + kImg3 + (wave * kGlds3 + q - kGlds3) * 1024);
-  };
   auto issue = [&](int kt) {
+    const bf16_t* pa = abase + (long)kt * kTK3 * g.lda;
+    const bf16_t* pb = bbase + (long)kt * kTK3 * g.ldb;
+    char* img = smem + (kt & (kRing3 - 1)) * kStage3;
 #pragma unroll
-    for (int q = 0; q < 2 * kGlds3; ++q) issue1(kt, q);
+    for (int i = 0; i < kGlds3; ++i) glds16_sv(pa, oa[i], img + (wave * kGlds3 + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < kGlds3; ++i) glds16_sv(pb, ob[i], img + kImg3 + (wave * kGlds3 + i) * 1024);
   };
   const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
   const int hq = fq | ((fg & 1) << 2);
@@ -310,23 +137,19 @@ __global__ __launch_bounds__(512, 1) void gemm_tn3_kernel(TnArgs g) {
   };
   // one step: MFMAs of stage kt (ca / cb) || fragments of stage kt + 1 (na / nb); refill; publish kt + 2
   auto step = [&](int kt, bfx8 (&ca)[8], bfx8 (&cb)[4], bfx8 (&na)[8], bfx8 (&nb)[4]) {
-    const bool refill = kt + 4 < nk;              // into stage kt's buffer (read during step kt - 1)
-    if (!SPREAD && refill) issue(kt + 4);
+    if (kt + 4 < nk) issue(kt + 4);               // into stage kt's buffer (read during step kt - 1)
     const bool nxt = kt + 1 < nk;
     const uint32_t nbase = lds0 + ((kt + 1) & (kRing3 - 1)) * kStage3;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
-      if (PRIO) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       if (nxt) {
         if (i < 4) nb[i] = tn_frag<0>(nbase, offn[i]);
         na[i] = tn_frag<0>(nbase, offm[i]);
       }
-      if (SPREAD && refill && (i & 1) == 0) issue1(kt + 4, i >> 1);
       __builtin_amdgcn_sched_barrier(0);
     }
     // publish stage kt + 2: this wave's DMAs of it landed (later stages may stay in flight), then the barrier
@@ -378,11 +201,11 @@ __global__ __launch_bounds__(512, 1) void gemm_tn3_kernel(TnArgs g) {
 }  // namespace
 
 bool dltb_gemm_tn_supported(int M, int N, int K) {
-  return M > 0 && N > 0 && K > 0 && M % kTM == 0 && N % kTN == 0 && K % kTK == 0 && K / kTK >= 2;
+  return M > 0 && N > 0 && K > 0 && M % kTM == 0 && N % kTN == 0 && K % (2 * kTK3) == 0 && K / kTK3 >= 4;
 }
 
 int dltb_gemm_tn(const void* a, const void* b, void* c, long lda, long ldb, long ldc, long sa, long sb, long sc,
-                 int M, int N, int K, int batch, int accumulate, hipStream_t st, int variant) {
+                 int M, int N, int K, int batch, int accumulate, hipStream_t st) {
   if (!dltb_gemm_tn_supported(M, N, K) || batch < 1) return -1;
   TnArgs g{};
   g.a = (const bf16_t*)a;
@@ -399,25 +222,13 @@ int dltb_gemm_tn(const void* a, const void* b, void* c, long lda, long ldb, long
   g.K = K;
   g.batch = batch;
   g.accumulate = accumulate;
-  constexpr int smem = 2 * kStage;
-  static_assert(kRing3 * kStage3 == smem, "V3 ring = the two V1/V2 stages");
-  int v = variant >= 1 && variant <= 5 ? variant : 3;
-  if (v >= 3 && (K % (2 * kTK3) != 0 || K / kTK3 < 4)) v = 2;   // the ring kernels step in pairs, fill 4 stages
-  static bool attr[5] = {false, false, false, false, false};
-  const void* fns[5] = {(const void*)gemm_tn_kernel<1>, (const void*)gemm_tn_kernel<2>,
-                        (const void*)gemm_tn3_kernel<true, false>, (const void*)gemm_tn3_kernel<true, true>,
-                        (const void*)gemm_tn3_kernel<false, false>};
-  if (!attr[v - 1]) {
-    (void)hipFuncSetAttribute(fns[v - 1], hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr[v - 1] = true;
+  constexpr int smem = kRing3 * kStage3;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_tn_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
   }
   const dim3 grid((unsigned)((long)(M / kTM) * (N / kTN) * batch));
-  switch (v) {
-    case 1: hipLaunchKernelGGL(gemm_tn_kernel<1>, grid, dim3(512), smem, st, g); break;
-    case 2: hipLaunchKernelGGL(gemm_tn_kernel<2>, grid, dim3(512), smem, st, g); break;
-    case 3: hipLaunchKernelGGL((gemm_tn3_kernel<true, false>), grid, dim3(512), smem, st, g); break;
-    case 4: hipLaunchKernelGGL((gemm_tn3_kernel<true, true>), grid, dim3(512), smem, st, g); break;
-    default: hipLaunchKernelGGL((gemm_tn3_kernel<false, false>), grid, dim3(512), smem, st, g); break;
-  }
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(512), smem, st, g);
   return 0;
 }

@@ -149,10 +149,11 @@ int dltb_gemm(const void* a, const void* b, void* c, const void* bias, float* pa
               long ldc, int M, int N, int K, bool tn, int accumulate, int splits, int cfg, int pf, int gm,
               const float* alpha, hipStream_t st, int stages = 0);
 
-// ---- gemm_tn.hip: C[b][M][N] (+)= A[b][K][M]^T B[b][K][N] (weight gradients dY^T X), bf16, 256 x 256 tiles
+// ---- gemm_tn.hip: C[b][M][N] (+)= A[b][K][M]^T B[b][K][N] (weight gradients dY^T X), bf16, 256 x 256 tiles,
+// M, N multiples of 256, K of 64 (>= 128)
 bool dltb_gemm_tn_supported(int M, int N, int K);
 int dltb_gemm_tn(const void* a, const void* b, void* c, long lda, long ldb, long ldc, long sa, long sb, long sc,
-                 int M, int N, int K, int batch, int accumulate, hipStream_t st, int variant = 3);
+                 int M, int N, int K, int batch, int accumulate, hipStream_t st);
 
 // ---- gemm_rs.hip: C[M,N] = A[M][K] B[N][K]^T (+bias) (+C), bf16, register-staged operands (the step's per-layer kernel)
 int dltb_gemm_rs_pick(int M, int N, int K);

@@ -67,21 +67,9 @@ def main():
                 else:
                     torch.mm(at, x, out=dw_ref)
 
-        def own1():
-            C.gemm_tn(dy, x, dw_own, False, 1)
-
-        def own2():
-            C.gemm_tn(dy, x, dw_own, False, 2)
-
         def own():
-            C.gemm_tn(dy, x, dw_own, False, 3)
-
-        def own4():
-            C.gemm_tn(dy, x, dw_own, False, 4)
-
-        def own5():
-            C.gemm_tn(dy, x, dw_own, False, 5)
-        t_lib, t_own1, t_own2, t_own, t_own4, t_own5 = graph_time([lib, own1, own2, own, own4, own5], a.iters)
+            C.gemm_tn(dy, x, dw_own, False)
+        t_lib, t_own = graph_time([lib, own], a.iters)
         lib()
         own()
         torch.cuda.synchronize()
@@ -91,7 +79,7 @@ def main():
         fl = 2.0 * B * M * N * K
         print(f"{name:11s} b{B:2d} M{M:6d} N{N:6d} K{K:6d}  hipBLASLt {t_lib:8.1f} us {fl / t_lib / 1e6:6.0f} TF/s "
               f"(err {e_lib:.3g})   own {t_own:8.1f} us {fl / t_own / 1e6:6.0f} TF/s (err {e_own:.3g})  "
-              f"x{t_lib / t_own:4.2f}  (v1 {t_own1:7.1f}, v2 {t_own2:7.1f}, v4 {t_own4:7.1f}, v5 {t_own5:7.1f} us)" + ("  MISMATCH" if e_own > 2 * e_lib + 0.05 else ""),
+              f"x{t_lib / t_own:4.2f}" + ("  MISMATCH" if e_own > 2 * e_lib + 0.05 else ""),
               flush=True)
         if name.startswith("dw."):
             tot[0] += t_lib
