@@ -562,6 +562,52 @@ DLTB_DEV uint32_t keep_mask_v(uint32_t mw, uint32_t bit) {
   return k;
 }
 
+// splits 1..KS-1 -> LDS -> split 0, then the scaled bf16 (or fp32 head-split partial) stores of split 0.
+// The caller guarantees no wave still reads the tile stages (the merge reuses the LDS from offset 0).
+template <int D, int KS, bool DROP>
+DLTB_DEV void dkdv_finish(const AttnArgs& P, char* smem, f32x16 (&dk)[D / 32], f32x16 (&dv)[D / 32], int kw,
+                          int sp, int lane, int h, int b, int hk, int key, int gs) {
+  constexpr int NACC = D / 32;
+  const int T = P.T;
+  if constexpr (KS > 1) {
+    constexpr int NF = 2 * 16 * NACC;
+    float* red0 = reinterpret_cast<float*>(smem) + kw * NF * 64 + lane;
+    if (sp > 0) {
+      float* red = red0 + (sp - 1) * 4 * NF * 64;
+#pragma unroll
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          red[(16 * dt + i) * 64] = dk[dt][i];
+          red[(16 * (NACC + dt) + i) * 64] = dv[dt][i];
+        }
+    }
+    __syncthreads();
+    if (sp > 0) return;
+#pragma unroll
+    for (int o = 0; o < KS - 1; ++o)
+#pragma unroll
+      for (int dt = 0; dt < NACC; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          dk[dt][i] += red0[o * 4 * NF * 64 + (16 * dt + i) * 64];
+          dv[dt][i] += red0[o * 4 * NF * 64 + (16 * (NACC + dt) + i) * 64];
+        }
+  }
+  const float s_drop = DROP ? P.drop_scale : 1.f;
+  if (P.gsplit > 1) {      // partial over this workgroup's heads -> fp32, summed by dkdv_reduce_kernel
+    const long plane = (long)P.B * T * P.Hkv * D;
+    float* pk = P.part + 2 * gs * plane + ((long)b * T + key) * P.Hkv * D + hk * D;
+    store_acc_rows_f32<D>(pk, dk, P.scale * s_drop, h);
+    store_acc_rows_f32<D>(pk + plane, dv, s_drop, h);
+    return;
+  }
+  bf16_t* dkrow = P.out + ((long)b * T + key) * P.out_stride + hk * D;
+  bf16_t* dvrow = P.out2 + ((long)b * T + key) * P.out2_stride + hk * D;
+  store_acc_rows<D>(dkrow, dk, P.scale * s_drop, h);
+  store_acc_rows<D>(dvrow, dv, s_drop, h);
+}
+
 template <int D, bool CAUSAL, bool DROP, int KS>
 __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   constexpr int TB = kTile * D * 2;
@@ -669,6 +715,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
   };
   load(0);
   store(0);
+  wait_vm<0>();        // this wave's LDS-DMA share landed (the compiler does not track the asm DMA)
   __syncthreads();
   for (int j = 0; j < njobs; ++j) {
     int g_, t;
@@ -778,45 +825,10 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(AttnArgs P) {
       }
     }
     if (j + 1 < njobs) store(j + 1);
+    wait_vm<0>();
     __syncthreads();
   }
-  if constexpr (KS > 1) {      // splits 1..KS-1 -> LDS -> split 0
-    constexpr int NF = 2 * 16 * NACC;
-    float* red0 = reinterpret_cast<float*>(smem) + kw * NF * 64 + lane;
-    if (sp > 0) {
-      float* red = red0 + (sp - 1) * 4 * NF * 64;
-#pragma unroll
-      for (int dt = 0; dt < NACC; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          red[(16 * dt + i) * 64] = dk[dt][i];
-          red[(16 * (NACC + dt) + i) * 64] = dv[dt][i];
-        }
-    }
-    __syncthreads();
-    if (sp > 0) return;
-#pragma unroll
-    for (int o = 0; o < KS - 1; ++o)
-#pragma unroll
-      for (int dt = 0; dt < NACC; ++dt)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          dk[dt][i] += red0[o * 4 * NF * 64 + (16 * dt + i) * 64];
-          dv[dt][i] += red0[o * 4 * NF * 64 + (16 * (NACC + dt) + i) * 64];
-        }
-  }
-  const float s_drop = DROP ? P.drop_scale : 1.f;
-  if (gsplit > 1) {      // partial over this workgroup's heads -> fp32, summed by dkdv_reduce_kernel
-    const long plane = (long)P.B * T * P.Hkv * D;
-    float* pk = P.part + 2 * gs * plane + ((long)b * T + key) * P.Hkv * D + hk * D;
-    store_acc_rows_f32<D>(pk, dk, P.scale * s_drop, h);
-    store_acc_rows_f32<D>(pk + plane, dv, s_drop, h);
-    return;
-  }
-  bf16_t* dkrow = P.out + ((long)b * T + key) * P.out_stride + hk * D;
-  bf16_t* dvrow = P.out2 + ((long)b * T + key) * P.out2_stride + hk * D;
-  store_acc_rows<D>(dkrow, dk, P.scale * s_drop, h);
-  store_acc_rows<D>(dvrow, dv, s_drop, h);
+  dkdv_finish<D, KS, DROP>(P, smem, dk, dv, kw, sp, lane, h, b, hk, key, gs);
 }
 
 // dK / dV = sum of the head-split partials (8 columns per thread), bf16 into the strided outputs
@@ -1161,6 +1173,7 @@ namespace {
 template <int D, bool C, bool DR>
 void launch_dkdv(const AttnArgs& a, hipStream_t st) {
   constexpr int KS = dkdv_ks<D>();
+
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, C, DR, KS>), dim3((a.T / kBlockRows) * a.B * a.Hkv * a.gsplit),
                      dim3(256 * KS), dkdv_smem_bytes<D>(), st, a);
   if (a.gsplit > 1) {

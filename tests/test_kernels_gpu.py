@@ -370,6 +370,9 @@ ATTN_CASES = [
     # causal GQA: the dK/dV pass splits each KV group's query heads over workgroups (fp32 partials)
     (1, 512, 8, 2, 128, True, 0.1),
     (2, 256, 4, 2, 64, True, 0.1),
+    # non-causal D = 64 (the pipelined dK/dV kernel): one query tile pair per split, and GQA (jobs over heads)
+    (1, 128, 2, 2, 64, False, 0.1),
+    (1, 512, 8, 2, 64, False, 0.1),
 ]
 
 
