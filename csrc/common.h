@@ -182,4 +182,13 @@ static inline uint32_t host_drop_threshold(float p) {
   return v > 65536u ? 65536u : v;
 }
 
+// XCD-grouped tile index of workgroup L in a grid of `tiles`: the dispatcher deals consecutive workgroups to
+// the 8 XCDs round robin, so XCD x = L & 7 gets the contiguous index range
+// [x (tiles / 8) + min(x, tiles % 8), ... + tiles / 8 + (x < tiles % 8)) -- neighbouring tiles (which share
+// operand slabs) meet in one XCD's L2.  A bijection on [0, tiles) for any tile count (performance only).
+DLTB_DEV int xcd_grouped(int L, int tiles) {
+  const int x = L & 7, q = tiles >> 3, r = tiles & 7;
+  return x * q + (x < r ? x : r) + (L >> 3);
+}
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

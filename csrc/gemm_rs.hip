@@ -243,8 +243,7 @@ __global__ __launch_bounds__(64 * NW * KG, 1) void gemm_rsf_kernel(RsArgs g) {
   // only), then groups of gm m-tiles x all n-tiles so an XCD's A and B panels share its L2
   const int tiles_n = g.N / BN, tiles_m = g.M / BM, tiles = tiles_m * tiles_n;
   const int L = blockIdx.x;
-  int idx = L;
-  if ((tiles & 7) == 0) idx = (L & 7) * (tiles >> 3) + (L >> 3);
+  const int idx = xcd_grouped(L, tiles);
   int mb, nb;
   if (g.gm > 1 && tiles_m % g.gm == 0) {
     const int span = g.gm * tiles_n, grp_ = idx / span, in = idx - grp_ * span;
