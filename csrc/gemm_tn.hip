@@ -6,7 +6,7 @@
 // (dY [T][out], X [T][in], both row-major), so neither operand is K-contiguous.  hipBLASLt runs that layout
 // 25-45 % slower than the K-contiguous one (profiles/gemm_layouts_r2.txt: 1.03-1.04 against 1.48-1.52
 // PFLOP/s on the same shapes; the TinyGPT-A window-wide batched dW at 1.07-1.17).  Here the operands
-// are staged as they lie -- 64 token rows x 256 feature columns per operand and k-step, filled by LDS-DMA
+// are staged as they lie -- 32 token rows x 256 feature columns per operand and k-step, filled by LDS-DMA
 // (global_load_lds_dwordx4, 1 KiB = two 512-byte rows per wave-instruction) -- and the MFMA fragments
 // are read TRANSPOSED out of LDS with ds_read_b64_tr_b16, which hands each lane 4 consecutive tokens of
 // one feature column: the layout costs no extra pass and no extra LDS traffic.

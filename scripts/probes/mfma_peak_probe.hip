@@ -28,6 +28,27 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
     }                                                                                         \
   } while (0)
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// the same with v_mfma_f32_16x16x32_bf16 (half the FLOP per instruction at half the cycles): 8 accumulators
+__global__ __launch_bounds__(512) void mfma16_loop(const uint4* __restrict__ src, float* __restrict__ out, int iters) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint4 a4 = src[(tid * 2) & 4095], b4 = src[(tid * 2 + 1) & 4095];
+  const bf16x8 a = __builtin_bit_cast(bf16x8, a4), b = __builtin_bit_cast(bf16x8, b4);
+  f32x4 c[8] = {};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        c[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16((q & 1) ? a : b, (q & 2) ? b : a, c[q], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s += c[q][0] + c[q][1] + c[q][2] + c[q][3];
+  out[tid] = s;
+}
+
 __global__ __launch_bounds__(512) void mfma_loop(const uint4* __restrict__ src, float* __restrict__ out, int iters) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4 a4 = src[(tid * 2) & 4095], b4 = src[(tid * 2 + 1) & 4095];
@@ -74,19 +95,22 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  const double flop = 2.0 * 32 * 32 * 16 * 16.0 * iters * (blocks * threads / 64.0);   // per launch
+  // per launch: 16 MFMAs of 32x32x16 per iteration and wave; the 16x16x32 loop issues 32 (same FLOP)
+  const double flop = 2.0 * 32 * 32 * 16 * 16.0 * iters * (blocks * threads / 64.0);
   for (int round = 0; round < 3; ++round) {
-    for (int z = 0; z < 2; ++z) {
-      const uint4* src = z ? d_zero : d_rand;
-      hipLaunchKernelGGL(mfma_loop, dim3(blocks), dim3(threads), 0, 0, src, d_out, iters / 4);   // warm
+    for (int z = 0; z < 4; ++z) {
+      const uint4* src = (z & 1) ? d_zero : d_rand;
+      auto kern = z < 2 ? mfma_loop : mfma16_loop;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, src, d_out, iters / 4);   // warm
       CHECK(hipEventRecord(e0));
-      for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(mfma_loop, dim3(blocks), dim3(threads), 0, 0, src, d_out, iters);
+      for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, src, d_out, iters);
       CHECK(hipEventRecord(e1));
       CHECK(hipEventSynchronize(e1));
       float ms = 0.f;
       CHECK(hipEventElapsedTime(&ms, e0, e1));
-      std::printf("round %d %-6s operands: %8.2f ms for 5 launches, %7.1f TFLOP/s bf16 (%d CUs, %d waves/CU)\n", round,
-                  z ? "zero" : "random", ms, 5.0 * flop / (ms * 1e-3) / 1e12, cus, threads / 64);
+      std::printf("round %d %s %-6s operands: %8.2f ms for 5 launches, %7.1f TFLOP/s bf16 (%d CUs, %d waves/CU)\n",
+                  round, z < 2 ? "32x32x16" : "16x16x32", (z & 1) ? "zero" : "random", ms, 5.0 * flop / (ms * 1e-3) / 1e12,
+                  cus, threads / 64);
     }
   }
   CHECK(hipGetLastError());
