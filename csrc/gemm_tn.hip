@@ -71,7 +71,9 @@ DLTB_DEV bfx8 tn_frag(uint32_t base, uint32_t off) {
 // at a step boundary.  (Measured against it on the dW shapes, profiles/gemm_tn_r6.txt: 64-deep k-steps in
 // two stage buffers with two barriers per step, 8-10 % slower; the same with one barrier and the second
 // substep's reads pipelined, 3-5 % slower; the refill's DMA spread over the MFMA groups and s_setprio
-// around them, within +-2 %.)
+// around them, within +-2 %; the loop made branch-free, -1.5 %.  Four waves of 128 x 128 outputs (one wave
+// per SIMD, 256 accumulator registers) did not compile without spills: hipcc shuttled the accumulators
+// between AGPRs and VGPRs inside the loop.)
 constexpr int kTK3 = 32;
 constexpr int kImg3 = kTK3 * kRowB;           // 16 KiB
 constexpr int kStage3 = 2 * kImg3;            // 32 KiB
@@ -103,9 +105,12 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
     ob[i] = (uint32_t)((row * g.ldb + col) * 2);
   }
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
+  // stage kt into ring slot kt & 3; past the last stage the source is clamped to it (a refill nobody reads,
+  // so the loop needs no branch and one uniform vmcnt wait per step)
   auto issue = [&](int kt) {
-    const bf16_t* pa = abase + (long)kt * kTK3 * g.lda;
-    const bf16_t* pb = bbase + (long)kt * kTK3 * g.ldb;
+    const int ks = min(kt, nk - 1);
+    const bf16_t* pa = abase + (long)ks * kTK3 * g.lda;
+    const bf16_t* pb = bbase + (long)ks * kTK3 * g.ldb;
     char* img = smem + (kt & (kRing3 - 1)) * kStage3;
 #pragma unroll
     for (int i = 0; i < kGlds3; ++i) glds16_sv(pa, oa[i], img + (wave * kGlds3 + i) * 1024);
@@ -134,10 +139,11 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) fa[i] = tn_frag<0>(base, offm[i]);
   };
-  // one step: MFMAs of stage kt (ca / cb) || fragments of stage kt + 1 (na / nb); refill; publish kt + 2
+  // one step: MFMAs of stage kt (ca / cb) || fragments of stage kt + 1 (na / nb); refill; publish kt + 2.
+  // Branch-free: the last step's reads of "stage nk" land in registers nobody uses, and the clamped refills
+  // keep the in-flight count uniform (stages kt + 3 and kt + 4 may stay in flight across the barrier).
   auto step = [&](int kt, bfx8 (&ca)[8], bfx8 (&cb)[4], bfx8 (&na)[8], bfx8 (&nb)[4]) {
-    if (kt + 4 < nk) issue(kt + 4);               // into stage kt's buffer (read during step kt - 1)
-    const bool nxt = kt + 1 < nk;
+    issue(kt + 4);                                // into stage kt's buffer (read during step kt - 1)
     const uint32_t nbase = lds0 + ((kt + 1) & (kRing3 - 1)) * kStage3;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -145,17 +151,11 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(cb[j], ca[i], acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
-      if (nxt) {
-        if (i < 4) nb[i] = tn_frag<0>(nbase, offn[i]);
-        na[i] = tn_frag<0>(nbase, offm[i]);
-      }
+      if (i < 4) nb[i] = tn_frag<0>(nbase, offn[i]);
+      na[i] = tn_frag<0>(nbase, offm[i]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // publish stage kt + 2: this wave's DMAs of it landed (later stages may stay in flight), then the barrier
-    const int later = min(nk - 1, kt + 4) - (kt + 2);     // stages issued after kt + 2
-    if (later >= 2) wait_vm<4 * kGlds3>();
-    else if (later == 1) wait_vm<2 * kGlds3>();
-    else wait_vm<0>();
+    wait_vm<4 * kGlds3>();                        // stage kt + 2 landed for this wave
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     tn_barrier();
     __builtin_amdgcn_sched_barrier(0);
