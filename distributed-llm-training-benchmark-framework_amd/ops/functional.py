@@ -570,8 +570,21 @@ def own_wgrad(dy, x, dw, accumulate):
     N = x.shape[-1]
     if not ext().gemm_tn_supported(M, N, K):
         return False
+    # 256 x 256 tiles, one workgroup per CU: below one tile per CU (a single layer's product, or the few-block
+    # dW batches of a gradient bucket at world > 1) hipBLASLt's smaller tiles / split-K fill the chip instead
+    if (M // 256) * (N // 256) * (dy.shape[0] if dy.dim() == 3 else 1) < _cu_count(dy.device):
+        return False
     ext().gemm_tn(dy, x, dw, bool(accumulate))
     return True
+
+
+_CUS = {}
+
+
+def _cu_count(dev):
+    if dev not in _CUS:
+        _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CUS[dev]
 
 
 def linear_wgrad(dy2d, x2d, dw, db, accumulate):
