@@ -137,10 +137,16 @@ def test_prediction_lookup_reads_the_newest_table():
     rows = [json.loads(ln) for ln in open(os.path.join(ROOT, newest)) if ln.strip()]
     rows = [r for r in rows if r.get("prediction")]
     assert rows
+    key = lambda r: (r["config"]["parallelism"], r["dtype"], r["emulated_world"], r["config"]["seq_len"],
+                     r["config"]["model"])
+    counts = {}
     for r in rows:
-        got = bench.predicted_row(r["config"]["parallelism"], r["dtype"], r["emulated_world"])
+        counts[key(r)] = counts.get(key(r), 0) + 1
+    for r in rows:
+        got = bench.predicted_row(*key(r))
         assert got is not None and got["table"] == newest, (r["config"]["parallelism"], got)
-        assert got["ms_per_step"] == r["ms_per_step"]
+        if counts[key(r)] == 1:        # (the M7B rows differ only in their DeepSpeed config file)
+            assert got["ms_per_step"] == r["ms_per_step"]
     # a round's "_final" table sorts before the same round's earlier one
     names = [os.path.basename(t) for t in tables]
     for i, n in enumerate(names):
