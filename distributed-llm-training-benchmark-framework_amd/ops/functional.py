@@ -559,7 +559,7 @@ _OWN_WGRAD = _os.environ.get("DLTB_OWN_WGRAD", "1") == "1"
 
 
 def own_wgrad(dy, x, dw, accumulate):
-    """dw (+)= dy^T x (2-D, or batched [b, T, *] views) on gemm_tn when the shapes and layouts fit; else False."""
+    """dw (+)= dy^T x for batched [b, T, *] views on gemm_tn when the shapes and layouts fit; else False."""
     if not (_OWN_WGRAD and dy.is_cuda and dy.dtype == x.dtype == dw.dtype and dy.dtype == torch.bfloat16
             and dy.dim() == x.dim() == dw.dim() and dy.dim() in (2, 3)):
         return False
@@ -570,9 +570,11 @@ def own_wgrad(dy, x, dw, accumulate):
     N = x.shape[-1]
     if not ext().gemm_tn_supported(M, N, K):
         return False
-    # 256 x 256 tiles, one workgroup per CU: below one tile per CU (a single layer's product, or the few-block
-    # dW batches of a gradient bucket at world > 1) hipBLASLt's smaller tiles / split-K fill the chip instead
-    if (M // 256) * (N // 256) * (dy.shape[0] if dy.dim() == 3 else 1) < _cu_count(dy.device):
+    # Batched products only, from one 256 x 256 tile per CU up.  Below one tile per CU (the few-block dW batches
+    # of a gradient bucket at world > 1) hipBLASLt's smaller tiles / split-K fill the chip; single products
+    # (the tied head's wgrad, Mistral-7B's per-layer dW) run on cold operands where hipBLASLt measured faster in
+    # the step: head 115 vs 121-138 us, M7B 200 vs 229 ms per window (profiles/gemm_tn_r6.txt)
+    if dy.dim() != 3 or dy.shape[0] < 2 or (M // 256) * (N // 256) * dy.shape[0] < _cu_count(dy.device):
         return False
     ext().gemm_tn(dy, x, dw, bool(accumulate))
     return True
