@@ -71,9 +71,10 @@ DLTB_DEV bfx8 tn_frag(uint32_t base, uint32_t off) {
 // at a step boundary.  (Measured against it on the dW shapes, profiles/gemm_tn_r6.txt: 64-deep k-steps in
 // two stage buffers with two barriers per step, 8-10 % slower; the same with one barrier and the second
 // substep's reads pipelined, 3-5 % slower; the refill's DMA spread over the MFMA groups and s_setprio
-// around them, within +-2 %; the loop made branch-free, -1.5 %.  Four waves of 128 x 128 outputs (one wave
-// per SIMD, 256 accumulator registers) did not compile without spills: hipcc shuttled the accumulators
-// between AGPRs and VGPRs inside the loop.)
+// around them, within +-2 %; the loop made branch-free, -1.5 %; four waves of 128 x 128 outputs (one wave per
+// SIMD, 64 MFMAs against 16 fragment reads per k-step, the 256 accumulators pinned in AGPRs by inline-asm
+// MFMAs), 2 % slower.  The MFMA stream alone, with this kernel's 8 x 4 distinct fragments and 32 accumulators
+// per wave, sustains 2.04 PF/s on random data (scripts/probes/mfma_peak_probe.hip).)
 constexpr int kTK3 = 32;
 constexpr int kImg3 = kTK3 * kRowB;           // 16 KiB
 constexpr int kStage3 = 2 * kImg3;            // 32 KiB

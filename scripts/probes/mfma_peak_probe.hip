@@ -49,6 +49,31 @@ __global__ __launch_bounds__(512) void mfma16_loop(const uint4* __restrict__ src
   out[tid] = s;
 }
 
+// the weight-gradient GEMM's inner loop without memory: 8 x 4 distinct operand fragments, 32 accumulators
+// (csrc/gemm_tn.hip step(): acc[i][j] = mfma(b[j], a[i], acc[i][j])) -- register-file operand traffic of a real tile
+__global__ __launch_bounds__(512) void mfma16_tile_loop(const uint4* __restrict__ src, float* __restrict__ out,
+                                                         int iters) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  bf16x8 a[8], b[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = __builtin_bit_cast(bf16x8, src[(tid * 12 + i) & 4095]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = __builtin_bit_cast(bf16x8, src[(tid * 12 + 8 + j) & 4095]);
+  f32x4 c[8][4] = {};
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], c[i][j], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += c[i][j][0] + c[i][j][1] + c[i][j][2] + c[i][j][3];
+  out[tid] = s;
+}
+
 __global__ __launch_bounds__(512) void mfma_loop(const uint4* __restrict__ src, float* __restrict__ out, int iters) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const uint4 a4 = src[(tid * 2) & 4095], b4 = src[(tid * 2 + 1) & 4095];
@@ -98,9 +123,9 @@ int main(int argc, char** argv) {
   // per launch: 16 MFMAs of 32x32x16 per iteration and wave; the 16x16x32 loop issues 32 (same FLOP)
   const double flop = 2.0 * 32 * 32 * 16 * 16.0 * iters * (blocks * threads / 64.0);
   for (int round = 0; round < 3; ++round) {
-    for (int z = 0; z < 4; ++z) {
+    for (int z = 0; z < 6; ++z) {
       const uint4* src = (z & 1) ? d_zero : d_rand;
-      auto kern = z < 2 ? mfma_loop : mfma16_loop;
+      auto kern = z < 2 ? mfma_loop : z < 4 ? mfma16_loop : mfma16_tile_loop;
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, src, d_out, iters / 4);   // warm
       CHECK(hipEventRecord(e0));
       for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, src, d_out, iters);
@@ -109,7 +134,8 @@ int main(int argc, char** argv) {
       float ms = 0.f;
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       std::printf("round %d %s %-6s operands: %8.2f ms for 5 launches, %7.1f TFLOP/s bf16 (%d CUs, %d waves/CU)\n",
-                  round, z < 2 ? "32x32x16" : "16x16x32", (z & 1) ? "zero" : "random", ms, 5.0 * flop / (ms * 1e-3) / 1e12,
+                  round, z < 2 ? "32x32x16" : z < 4 ? "16x16x32" : "16x16x32 tile (8x4 frags)", (z & 1) ? "zero" : "random",
+                  ms, 5.0 * flop / (ms * 1e-3) / 1e12,
                   cus, threads / 64);
     }
   }
