@@ -106,17 +106,42 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_kernel(TnArgs g) {
     ob[i] = (uint32_t)((row * g.ldb + col) * 2);
   }
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem;
-  // stage kt into ring slot kt & 3; past the last stage the source is clamped to it (a refill nobody reads,
-  // so the loop needs no branch and one uniform vmcnt wait per step)
+  // stage kt into ring slot kt & 3: the wave's 2 + 2 LDS-DMA pieces from ONE asm block (m0 saved once, the four
+  // destinations as immediates off the slot base), the sources as running wave-uniform pointers advanced one stage
+  // per issue and clamped at the last stage (a refill nobody reads: the loop needs no branch and one uniform vmcnt
+  // wait per step).  The per-piece form spent ~55 scalar instructions per step on 64-bit address products,
+  // generic -> LDS pointer conversions and m0 save / restore.
+  static_assert(kGlds3 == 2 && kImg3 == 0x4000, "issue() hard-codes two 1 KiB pieces per operand");
+  const uint64_t astride = (uint64_t)kTK3 * g.lda * 2, bstride = (uint64_t)kTK3 * g.ldb * 2;
+  uint64_t pa = uniform_ptr(abase), pb = uniform_ptr(bbase);   // stage to issue next
+  const uint32_t ldsw = lds0 + (uint32_t)(wave * kGlds3 * 1024);
   auto issue = [&](int kt) {
-    const int ks = min(kt, nk - 1);
-    const bf16_t* pa = abase + (long)ks * kTK3 * g.lda;
-    const bf16_t* pb = bbase + (long)ks * kTK3 * g.ldb;
-    char* img = smem + (kt & (kRing3 - 1)) * kStage3;
-#pragma unroll
-    for (int i = 0; i < kGlds3; ++i) glds16_sv(pa, oa[i], img + (wave * kGlds3 + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < kGlds3; ++i) glds16_sv(pb, ob[i], img + kImg3 + (wave * kGlds3 + i) * 1024);
+    const uint32_t lds = ldsw + (uint32_t)((kt & (kRing3 - 1)) * kStage3);
+    // destinations computed outside the asm: an s_add inside it would clobber SCC under a live compare
+    const uint32_t l1 = lds + 0x400, l2 = lds + 0x4000, l3 = lds + 0x4400;
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %[keep], m0\n\t"
+        "s_mov_b32 m0, %[l0]\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[va0], %[sa]\n\t"
+        "s_mov_b32 m0, %[l1]\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[va1], %[sa]\n\t"
+        "s_mov_b32 m0, %[l2]\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[vb0], %[sb]\n\t"
+        "s_mov_b32 m0, %[l3]\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %[vb1], %[sb]\n\t"
+        "s_mov_b32 m0, %[keep]"
+        : [keep] "=&s"(keep)
+        : [va0] "v"(oa[0]), [va1] "v"(oa[1]), [vb0] "v"(ob[0]), [vb1] "v"(ob[1]), [sa] "s"(pa), [sb] "s"(pb),
+          [l0] "s"(lds), [l1] "s"(l1), [l2] "s"(l2), [l3] "s"(l3)
+        : "memory");
+    const bool more = kt + 1 < nk;                // advance unless this was the last real stage
+    pa += more ? astride : 0;
+    pb += more ? bstride : 0;
   };
   const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
   const int hq = fq | ((fg & 1) << 2);
