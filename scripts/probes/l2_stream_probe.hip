@@ -68,6 +68,57 @@ __global__ __launch_bounds__(256, 1) void probe_dma(const char* buf, long stride
   if (tid == 0) sink[blockIdx.x] = smem[lane];
 }
 
+// mode 3 (round 6): the DMA ring issued the way csrc/gemm_tn.hip does it -- wave-uniform base pointer + per-lane 32-bit
+// offsets (saddr form), LDS destinations precomputed, two pieces per asm block with m0 saved once
+__device__ __forceinline__ void glds16x2(uint64_t sbase, uint32_t v0, uint32_t v1, uint32_t l0, uint32_t l1) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\t"
+               "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(v0), "v"(v1), "s"(sbase), "s"(l0), "s"(l1)
+               : "memory");
+}
+
+template <int ROWS, int NSTAGE>
+__global__ __launch_bounds__(256, 1) void probe_dma_sv(const char* buf, long stride, long panel, int steps,
+                                                      int* sink) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NI = ROWS * 8 / 256;
+  static_assert(NI % 2 == 0, "pieces come in pairs");
+  constexpr int STAGE = ROWS * 128;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const char* base = buf + (long)(blockIdx.x % 64) * panel;
+  uint32_t off[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int lin = (w * NI + i) * 64 + lane, row = lin >> 3, ch = lin & 7;
+    off[i] = (uint32_t)(row * stride + ch * 16);
+  }
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) char*)smem + (uint32_t)(w * NI * 1024);
+  auto load = [&](int s, int slot) {
+    const uint64_t b = (uint64_t)(uintptr_t)(base + (long)(s & 15) * 128);
+    const uint64_t sb = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t l = lds0 + (uint32_t)(slot * STAGE);
+#pragma unroll
+    for (int i = 0; i < NI; i += 2) glds16x2(sb, off[i], off[i + 1], l + i * 1024, l + (i + 1) * 1024);
+  };
+  for (int s = 0; s < NSTAGE - 1; ++s) load(s, s);
+  int slot = 0;
+  for (int s = 0; s < steps; ++s) {
+    const int ahead = min(steps - 1 - s, NSTAGE - 2);
+    if (ahead >= NSTAGE - 2) wait_vm<(NSTAGE - 2) * NI>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (s + NSTAGE - 1 < steps) load(s + NSTAGE - 1, slot == 0 ? NSTAGE - 1 : slot - 1);
+    slot = slot == NSTAGE - 1 ? 0 : slot + 1;
+  }
+  wait_vm<0>();
+  __syncthreads();
+  if (tid == 0) sink[blockIdx.x] = smem[lane];
+}
+
 template <int ROWS, int DEPTH, bool WRITE>
 __global__ __launch_bounds__(256, 1) void probe_reg(const char* buf, long stride, long panel, int steps,
                                                    int* sink) {
@@ -149,6 +200,10 @@ int main() {
         {probe_dma<192, 6>, 6 * 192 * 128, 192, "dma  rows192 nstage6"},
         {probe_dma<128, 8>, 8 * 128 * 128, 128, "dma  rows128 nstage8"},
         {probe_dma<256, 4>, 4 * 256 * 128, 256, "dma  rows256 nstage4"},
+        {probe_dma_sv<192, 4>, 4 * 192 * 128, 192, "dma-sv rows192 nstage4"},
+        {probe_dma_sv<192, 6>, 6 * 192 * 128, 192, "dma-sv rows192 nstage6"},
+        {probe_dma_sv<128, 8>, 8 * 128 * 128, 128, "dma-sv rows128 nstage8"},
+        {probe_dma_sv<256, 4>, 4 * 256 * 128, 256, "dma-sv rows256 nstage4"},
         {probe_reg<192, 2, false>, 0, 192, "reg  rows192 depth2"},
         {probe_reg<192, 4, false>, 0, 192, "reg  rows192 depth4"},
         {probe_reg<128, 6, false>, 0, 128, "reg  rows128 depth6"},
