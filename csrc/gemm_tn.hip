@@ -73,7 +73,8 @@ DLTB_DEV bfx8 tn_frag(uint32_t base, uint32_t off) {
 // substep's reads pipelined, 3-5 % slower; the refill's DMA spread over the MFMA groups and s_setprio
 // around them, within +-2 %; the loop made branch-free, -1.5 %; four waves of 128 x 128 outputs (one wave per
 // SIMD, 64 MFMAs against 16 fragment reads per k-step, the 256 accumulators pinned in AGPRs by inline-asm
-// MFMAs), 2 % slower.  The MFMA stream alone, with this kernel's 8 x 4 distinct fragments and 32 accumulators
+// MFMAs), 2 % slower; v_mfma_f32_32x32x16 (16 instead of 32 MFMAs per wave and k-step for the same reads, twice
+// the issue cycles between them; 64-byte-segment swizzle), 2 % slower.  The MFMA stream alone, with this kernel's 8 x 4 distinct fragments and 32 accumulators
 // per wave, sustains 2.04 PF/s on random data (scripts/probes/mfma_peak_probe.hip).)
 constexpr int kTK3 = 32;
 constexpr int kImg3 = kTK3 * kRowB;           // 16 KiB
