@@ -165,9 +165,10 @@ class _BlockFn(torch.autograd.Function):
         return x1, m
 
     @staticmethod
-    def backward(ctx, dx2, dm_unused):
-        # dx2 = d(x1 + Dropout(m)) from the consumer; m's gradient (Dropout backward, with the fc2
-        # bias column sum) is formed here
+    def backward(ctx, dx2, dm_in):
+        # dx2 = d(x1 + Dropout(m)) from the consumer.  m's gradient (Dropout backward, with the fc2
+        # bias column sum) comes from the consumer block's LN1 backward kernel (dm_in, engines whose
+        # gradient slots may be written ahead) or is formed here
         model, i = ctx.model, ctx.i
         rt, unit = model.rt, model.unit_blocks[i]
         (x, h1, mean1, rstd1, qkv, o, lse, amask, x1, h2, mean2, rstd2, f, g) = ctx.saved
@@ -193,8 +194,11 @@ class _BlockFn(torch.autograd.Function):
         shared = rt.grad_reducer()
         red = shared if shared is not None else F_.GradReducer()
         # MLP
-        dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
-                                 out=lb and lb.dm)
+        if dm_in is not None:
+            dm = dm_in
+        else:
+            dm = F_.dropout_bwd_bias(dx2, p, rt.seed, model.site_mlp(i), s[11][0], s[11][1], red,
+                                     out=lb and lb.dm)
         wgrad(10, dm, g, ("dm", "g"))
         w2t = rt.weight_t(unit, 10, w2)
         df = None
@@ -218,13 +222,24 @@ class _BlockFn(torch.autograd.Function):
         wgrad(2, dqkv, h1, ("dqkv", "h1"))
         wint = rt.weight_t(unit, 2, win)
         dh1 = F_.linear_dgrad(dqkv, win, wint)
+        drop_prev = None
+        if ctx.fused_prev and rt.grad_write_ahead and dx2.is_cuda:
+            # the previous block's Dropout(m') backward and fc2 bias partials, formed with dx by the
+            # LN1 backward kernel (one colpart launch less per layer: -0.6 % per micro-step,
+            # profiles/fused_dropout_bwd_ab_r6.txt)
+            ps = rt.grad_slot(model.unit_blocks[i - 1], 11)
+            plb = model.layer_buffer(i - 1) if lb is not None else None
+            drop_prev = (p, rt.seed, model.site_mlp(i - 1), plb and plb.dm, ps[0], ps[1])
         dx = F_.norm_bwd(dh1, x, ln1w, mean1, rstd1, dx1, s[0][0], s[1][0], s[0][1], False,
-                         red, bias=(dqkv, s[3][0], s[3][1]))
+                         red, bias=(dqkv, s[3][0], s[3][1]), drop=drop_prev)
+        dm_prev = None
+        if drop_prev is not None:
+            dx, dm_prev = dx
         if shared is None:
             red.flush()
         rt.grads_ready(unit)
         rt.release_backward(unit)
-        return dx, None, None, None
+        return dx, dm_prev, None, None
 
 
 class _HeadFn(torch.autograd.Function):

@@ -280,20 +280,32 @@ def gelu_bwd(dg, f, db, accumulate, red=None, out=None):
         if red is None:
             return _into(out, ext().gelu_bwd(dg, f, db, accumulate))
         df = torch.empty_like(dg) if out is None else out
-        parts = ext().colpart([_GELU], [dg], [f], [df], [None], [None], 0.0, None, [0])
+        extra = _take_row_matched(red, dg, 2)        # deferred plain sums ride along (same row count)
+        n = len(extra)
+        parts = ext().colpart([_GELU] + [_PLAIN] * n, [dg] + [e[0] for e in extra], [f] + [None] * n,
+                              [df] + [None] * n, [None] * (n + 1), [None] * (n + 1), 0.0, None, [0] * (n + 1))
         red.add(parts[0][0], db, accumulate)
+        for (src, o, acc), pt in zip(extra, parts[1:]):
+            red.add(pt[0], o, acc)
         return df
     return _into(out, ref.gelu_bwd(dg, f, db, accumulate))
+
+
+def _take_row_matched(red, t, limit):
+    """Up to ``limit`` of the reducer's deferred plain column sums whose source has ``t``'s row count
+    (colpart segments must share it); they are removed from ``red.pending``."""
+    rows, keep, extra = t.numel() // t.shape[-1], [], []
+    for e in red.pending:
+        (extra if len(extra) < limit and e[0].numel() // e[0].shape[-1] == rows else keep).append(e)
+    red.pending = keep
+    return extra
 
 
 def dropout_bwd_bias(g, p, seed, site, db, accumulate, red, out=None):
     """dm = dropout_mask(g) / (1-p) (the Dropout backward) with colsum(dm) -> db fused."""
     if _gpu(g):
         dm = torch.empty_like(g) if out is None else out
-        rows, keep, extra = g.numel() // g.shape[-1], [], []
-        for e in red.pending:               # colpart segments must share the row count
-            (extra if len(extra) < 2 and e[0].numel() // e[0].shape[-1] == rows else keep).append(e)
-        red.pending = keep
+        extra = _take_row_matched(red, g, 2)
         n = len(extra)
         parts = ext().colpart([_DROP] + [_PLAIN] * n, [g] + [e[0] for e in extra], [None] * (n + 1),
                               [dm] + [None] * n, [None] * (n + 1), [None] * (n + 1), p,

@@ -42,11 +42,21 @@ def main():
     s_, y, mean, rstd = C.norm_fwd(x, r, w, b, 1e-5, False, 0.0, None, 0)
     df, dm = torch.empty_like(dg), torch.empty_like(dy)
     out = torch.empty(f, **bf)
+    half = (1 * 16 * (M // 64) * 2) // 2
+    mask = C.norm_fwd_mask(x, r, w, b, 1e-5, False, 0.1, seed, 2, None, 1, M, 16, 0.1, 5, None, 0, half)[4]
     parts = C.colpart([_LN, _PLAIN], [dy, dq], [x, None], [None, None], [mean, None], [rstd, None], 0.0, None, [0, 0])
     rows = [
         ("norm_fwd (LN)", lambda: C.norm_fwd(x, None, w, b, 1e-5, False, 0.0, None, 0), 8),
         ("norm_fwd (LN + residual)", lambda: C.norm_fwd(x, r, w, b, 1e-5, False, 0.0, None, 0), 16),
+        ("norm_fwd_mask (LN+res, half mask)", lambda: C.norm_fwd_mask(x, r, w, b, 1e-5, False, 0.1, seed, 2, None, 1, M, 16,
+                                                                    0.1, 5, mask, 0, half), 20),
+        ("norm_fwd_mask (LN+res, other half)", lambda: C.norm_fwd_mask(x, r, w, b, 1e-5, False, 0.0, seed, 0, None, 1, M, 16,
+                                                                     0.1, 5, mask, half, -1), 20),
         ("norm_bwd_dx (+dres)", lambda: C.norm_bwd_dx(dy, x, w, mean, rstd, r, False), 16),
+        ("norm_bwd_fused (+dres, dx sum)", lambda: C.norm_bwd_fused(dy, x, w, mean, rstd, r, False, True, None, None,
+                                                                    0.0, None, 0), 16),
+        ("norm_bwd_fused (+dres, drop)", lambda: C.norm_bwd_fused(dy, x, w, mean, rstd, r, False, False, None, dm, 0.1,
+                                                                  seed, 4), 20),
         ("gelu_fwd", lambda: C.gelu_fwd(ff), 32),
         ("dropout add", lambda: C.dropout(x, r, 0.1, seed, 3), 12),
         ("colpart DROP", lambda: C.colpart([_DROP], [dy], [None], [dm], [None], [None], 0.1, seed, [3]), 8),

@@ -93,6 +93,36 @@ def test_split_mask_generation_is_bitwise_identical():
         assert torch.equal(outs[0][1][n], outs[1][1][n]), n
 
 
+def test_fused_dropout_backward_matches_producer_side():
+    """With grad_write_ahead (the replicated engines) block i+1's LN1 backward kernel forms block i's
+    MLP Dropout backward and fc2 bias partials (models/tinygpt.py); every gradient must match the
+    producer-side colpart path: dm is bitwise the same, the fc2 bias sums differ only in the grouping
+    of their fp32 partials."""
+    torch.manual_seed(0)
+    cfg = _cfg(T=256, layers=3)
+    ref_m = build_model(cfg).to("cuda", torch.bfloat16)
+    outs = []
+    for ahead in (False, True):
+        m = copy.deepcopy(ref_m)
+        m.rt = ParamRuntime()
+        m.rt.grad_write_ahead = ahead
+        s = StepSeed(5, device="cuda")
+        s.next()
+        m.rt.seed = s
+        m.train()
+        idx = torch.randint(0, cfg.vocab_size, (2, cfg.block_size), generator=torch.Generator().manual_seed(4))
+        _, loss = m(idx.cuda(), idx.cuda())
+        loss.backward()
+        outs.append((loss.detach(), {n: p.grad.clone() for n, p in m.named_parameters()}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    for n, g0 in outs[0][1].items():
+        g1 = outs[1][1][n]
+        if n.endswith("mlp.2.bias"):                      # fc2 bias
+            assert rel(g1, g0) < 1e-2, (n, rel(g1, g0))
+        else:
+            assert rel(g1, g0) < 1e-6, (n, rel(g1, g0))
+
+
 @pytest.mark.parametrize("strategy", ["zero3", "fsdp"])
 def test_sharded_world1_shared_column_reducer(strategy, monkeypatch):
     """ZeRO-3 / FSDP at world 1 send every block's bias / norm-weight column sums to one shared reducer
