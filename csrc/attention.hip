@@ -22,7 +22,7 @@
 // free (D=64: chunk ^ (((r>>1)&1)<<2 | (r>>2)&3); D=128: chunk ^ ((r&3)<<2 | (r>>2)&3)).
 // K/V (or Q/dO) tiles are double-buffered: global loads for tile t+1 are issued into registers
 // before the MFMA work on tile t and written to LDS after it.
-// Dropout uses the counter hash of common.h (row = (b*Hq + h)*T + q, col = key).  The keep-mask is
+// Dropout uses the attention-site counter hash of common.h (rng_attn_pair; row = (b*Hq + h)*T + q, col = key).  The keep-mask is
 // generated ONCE per call by a full-occupancy kernel as packed bits laid out for the forward's lane
 // mapping: word (bh, t, h, q) holds, in bit 16n + i, the decision for key 64t + 32n + (i&3) +
 // 8(i>>2) + 4h of query q — so forward and dQ lanes read one coalesced word per 64-key tile and the

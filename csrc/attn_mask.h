@@ -19,16 +19,25 @@ constexpr uint32_t mask_bit(int n, int i) {
   return (uint32_t)((i & 1) ? 31 - (8 * n + (i >> 1)) : 15 - (8 * n + (i >> 1)));
 }
 
-// one thread = one query row q of tile group g = (bh * nT + t) * 2 + h; 32 keep decisions
+// one thread = one query row q of tile group g = (bh * nT + t) * 2 + h; 32 keep decisions.  g is
+// uniform over the calling block (both callers), and every thread of the block must call: the 16
+// column-pair keys of the tile are mixed once per block (16 lanes, one VALU pass) and read from LDS.
 DLTB_DEV void attn_mask_word(uint32_t* __restrict__ mask, int T, uint32_t thr16, const int64_t* __restrict__ seed_ptr,
                              int64_t site, int q, uint32_t g) {
-  if (q >= T) return;
+  __shared__ __attribute__((aligned(16))) uint32_t ckey[16];
   const int nT = T / kMaskKeyTile;
   const int h = g & 1;
   const int t = (g >> 1) % nT;
   const uint32_t bh = (g >> 1) / nT;
   const uint64_t seed = site_seed(seed_ptr, site);
-  const uint32_t rk = rng_row_key(seed, bh * (uint32_t)T + q);
+  if (threadIdx.x < 16) {                  // pair k: register pair j = k of key sub-tile n = k / 8
+    const int k = threadIdx.x, n = k >> 3, i = 2 * (k & 7);
+    ckey[k] = rng_attn_col_key(seed, (uint32_t)(t * kMaskKeyTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h));
+  }
+  __syncthreads();
+  if (q >= T) return;
+  uint32_t rk = rng_row_key(seed, bh * (uint32_t)T + q);
+  asm("" : "+v"(rk));     // materialised once (else its last xor-shift is re-done per pair)
   uint32_t bits = 0xFFFFFFFFu;                               // thr16 == 0: keep everything
   if (thr16 != 0) {
     // one hash covers a key pair (i, i+1) of register pair j = 8n + i/2, whose keep bits live at
@@ -36,17 +45,23 @@ DLTB_DEV void attn_mask_word(uint32_t* __restrict__ mask, int T, uint32_t thr16,
     // min'ed with 1 gives 0 / 1 per half, shifted into place by one v_lshl_or_b32
     const uint32_t tm2 = (thr16 - 1u) * 0x10001u, one2 = 0x10001u;
     bits = 0;
+    const uint4* ck4 = reinterpret_cast<const uint4*>(ckey);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        const uint32_t key = (uint32_t)(t * kMaskKeyTile + 32 * n + (i & 3) + 8 * (i >> 2) + 4 * h);
-        const uint32_t hsh = rng_pair(rk, rng_col_key(seed, key));
-        uint32_t kk;
-        asm("v_pk_sub_u16 %0, %1, %2 clamp\n\tv_pk_min_u16 %0, %0, %3"
-            : "=&v"(kk) : "v"(hsh), "v"(tm2), "v"(one2));
-        static_assert(mask_bit(0, 1) == mask_bit(0, 0) + 16, "pair bits 16 apart");
-        bits |= kk << mask_bit(n, i);
+      for (int c = 0; c < 2; ++c) {
+        const uint4 ck = ck4[2 * n + c];                       // keys of pairs 8n + 4c .. + 3
+        const uint32_t cks[4] = {ck.x, ck.y, ck.z, ck.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 2 * (4 * c + e);
+          const uint32_t hsh = rng_attn_pair(rk, cks[e]);
+          uint32_t kk;
+          asm("v_pk_sub_u16 %0, %1, %2 clamp\n\tv_pk_min_u16 %0, %0, %3"
+              : "=&v"(kk) : "v"(hsh), "v"(tm2), "v"(one2));
+          static_assert(mask_bit(0, 1) == mask_bit(0, 0) + 16, "pair bits 16 apart");
+          bits |= kk << mask_bit(n, i);
+        }
       }
   }
   mask[(size_t)g * T + q] = bits;

@@ -169,6 +169,15 @@ DLTB_DEV uint32_t rng_col_key(uint64_t seed, uint32_t col) {
 }
 // hash covering the column pair (col & ~1, col | 1)
 DLTB_DEV uint32_t rng_pair(uint32_t row_key, uint32_t col_key) { return fmix32(row_key ^ col_key); }
+// Attention-probability dropout (the packed mask of attn_mask.h, 2/3 of all dropout decisions of a TinyGPT
+// step): the column key is mixed by its own fmix32 -- wave-uniform in the mask generators, so scalar ALU work --
+// and each (row, column pair) needs ONE multiply-xorshift round on the two independent 32-bit hashes: 3 VALU
+// per pair instead of fmix32's 6 (ops/rng.py attn_keep_mask; the statistical checks are in tests/test_ref_ops.py)
+DLTB_DEV uint32_t rng_attn_col_key(uint64_t seed, uint32_t col) { return fmix32(rng_col_key(seed, col)); }
+DLTB_DEV uint32_t rng_attn_pair(uint32_t row_key, uint32_t col_mixed) {
+  const uint32_t h = (row_key ^ col_mixed) * 0x85EBCA6Bu;
+  return h ^ (h >> 16);
+}
 DLTB_DEV bool rng_keep(uint32_t x, uint32_t col, uint32_t thr16) {
   uint32_t r = (col & 1u) ? (x >> 16) : (x & 0xFFFFu);
   return r >= thr16;

@@ -11,7 +11,7 @@ import math
 import torch
 import torch.nn.functional as F
 
-from .rng import keep_mask, keep_mask_2d, site_seed
+from .rng import attn_keep_mask, keep_mask, keep_mask_2d, site_seed
 
 
 def _f(t):
@@ -205,7 +205,7 @@ def _attn_keep(B, Hq, T, p, seed, site, device):
     s = _seed(seed, site)
     rows = torch.arange(B * Hq * T, dtype=torch.int64, device=device)[:, None]
     cols = torch.arange(T, dtype=torch.int64, device=device)[None, :]
-    return keep_mask(s, rows, cols, p).view(B, Hq, T, T)
+    return attn_keep_mask(s, rows, cols, p).view(B, Hq, T, T)
 
 
 def attn_fwd(q, k, v, B, T, Hq, Hkv, scale, causal, p, seed, site):

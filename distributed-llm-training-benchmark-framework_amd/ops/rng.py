@@ -11,8 +11,9 @@ so the MI355X kernels use a cheaper counter hash instead:
     keep    = r16 >= thr16,   thr16 = round(p * 65536)
 
 ``fmix32`` is the MurmurHash3 finaliser (a bijective avalanche mixer).  One hash yields the
-decisions for two adjacent columns and ``row_key`` is hoisted per row, so the attention kernel
-pays ~3 VALU ops per probability.  Every dropout site views its tensor as ``[rows, cols]`` and
+decisions for two adjacent columns and ``row_key`` is hoisted per row.  The attention-probability
+mask (T x T decisions per head) uses :func:`attn_keep_mask`, which mixes the column key on its own and
+combines the two keys with one multiply-xorshift round (3 VALU ops per column pair instead of 6).  Every dropout site views its tensor as ``[rows, cols]`` and
 gets its own 64-bit seed ``site_seed(step_seed, site)``; the backward kernels regenerate the
 identical mask instead of storing it.
 """
@@ -63,6 +64,21 @@ def keep_mask(seed: int, rows: torch.Tensor, cols: torch.Tensor, p: float) -> to
     s_hi = (seed >> 32) & MASK32
     rk = _fmix32((_mul32(rows, C_ROW) + s_hi) & MASK32)
     x = _fmix32(rk ^ ((_mul32(cols >> 1, C_COL) + s_lo) & MASK32))
+    r16 = torch.where((cols & 1) == 1, x >> 16, x & 0xFFFF)
+    return r16 >= drop_threshold(p)
+
+
+def attn_keep_mask(seed: int, rows: torch.Tensor, cols: torch.Tensor, p: float) -> torch.Tensor:
+    """Keep-mask of the attention-probability dropout (csrc/common.h ``rng_attn_pair``): the same row key,
+    the column-pair key mixed by its own ``fmix32``, and one multiply-xorshift round per (row, pair) --
+    ``x = (rk ^ fmix32(ck)) * 0x85EBCA6B; x ^= x >> 16``.  Half the per-pair VALU of ``keep_mask`` for the
+    T x T decisions per head, which dominate a step's dropout work."""
+    s_lo = seed & MASK32
+    s_hi = (seed >> 32) & MASK32
+    rk = _fmix32((_mul32(rows, C_ROW) + s_hi) & MASK32)
+    ck = _fmix32((_mul32(cols >> 1, C_COL) + s_lo) & MASK32)
+    x = _mul32(rk ^ ck, 0x85EBCA6B)
+    x = x ^ (x >> 16)
     r16 = torch.where((cols & 1) == 1, x >> 16, x & 0xFFFF)
     return r16 >= drop_threshold(p)
 

@@ -549,7 +549,7 @@ def test_norm_fwd_mask_fused_matches_separate(with_res):
 
 
 def test_attn_mask_words_match_reference():
-    """The packed attention-dropout words are bit-exact with ops/rng.py keep_mask: word
+    """The packed attention-dropout words are bit-exact with ops/rng.py attn_keep_mask: word
     (bh, t, h, q) bit mask_bit(n, i) <-> key 64t + 32n + (i&3) + 8(i>>2) + 4h (csrc/attn_mask.h)."""
     from dltb.ops import rng
     C = ext()
@@ -571,6 +571,6 @@ def test_attn_mask_words_match_reference():
     s = rng.site_seed(int(sd.value), site)
     rows = torch.arange(B * H * T, dtype=torch.int64, device=DEV)[:, None]
     cols = torch.arange(T, dtype=torch.int64, device=DEV)[None, :]
-    want = rng.keep_mask(s, rows, cols, p).view(B * H, T, T)
+    want = rng.attn_keep_mask(s, rows, cols, p).view(B * H, T, T)
     assert torch.equal(got, want)
 

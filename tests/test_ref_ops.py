@@ -33,6 +33,39 @@ def test_rng_properties():
     assert torch.equal(sub, keep[100:110])
 
 
+@pytest.mark.parametrize("site", [5, 6])
+def test_attention_mask_hash_statistics(site):
+    """attn_keep_mask (one multiply-xorshift round on two independently mixed keys, csrc/common.h
+    rng_attn_pair): keep rate, neighbour correlations, byte uniformity, and the rectangle statistic that
+    a plain XOR of row and column keys fails (k(r,c) k(r,c') k(r',c) k(r',c') centred: ~0.05 for XOR)."""
+    s = rng.site_seed(2024, site)
+    R, C = 1024, 2048
+    rows = torch.arange(R, dtype=torch.int64)[:, None]
+    cols = torch.arange(C, dtype=torch.int64)[None, :]
+    keep = rng.attn_keep_mask(s, rows, cols, 0.1).double()
+    assert abs(keep.mean().item() - (1 - 6554 / 65536)) < 0.003
+    k = keep - keep.mean()
+    var = k.var()
+    assert abs(((k[:, :-1] * k[:, 1:]).mean() / var).item()) < 0.01          # column pair halves, neighbours
+    assert abs(((k[:-1] * k[1:]).mean() / var).item()) < 0.01                  # neighbouring rows
+    g = torch.Generator().manual_seed(site)
+    ra, rb = torch.randint(0, R, (200000,), generator=g), torch.randint(0, R, (200000,), generator=g)
+    ca, cb = torch.randint(0, C, (200000,), generator=g), torch.randint(0, C, (200000,), generator=g)
+    rect = ((k[ra, ca] * k[ra, cb] * k[rb, ca] * k[rb, cb]).mean() / var ** 2).item()
+    assert abs(rect) < 0.015, rect
+    # the raw 16-bit values behind the decisions: uniform top bytes (chi-square, 255 dof)
+    rk = rng._fmix32((rng._mul32(rows, rng.C_ROW) + ((s >> 32) & rng.MASK32)) & rng.MASK32)
+    ck = rng._fmix32((rng._mul32(cols >> 1, rng.C_COL) + (s & rng.MASK32)) & rng.MASK32)
+    h = rng._mul32(rk ^ ck, 0x85EBCA6B)
+    h = h ^ (h >> 16)
+    r16 = torch.where((cols & 1) == 1, h >> 16, h & 0xFFFF)
+    hist = torch.bincount((r16 >> 8).flatten(), minlength=256).double()
+    e = R * C / 256
+    chi2 = (((hist - e) ** 2) / e).sum().item()
+    assert chi2 < 255 + 6 * math.sqrt(2 * 255), chi2
+    assert torch.equal(r16 >= 6554, keep.bool())
+
+
 def test_mul32_matches_uint32():
     a = torch.tensor([0, 1, 0xFFFFFFFF, 0x12345678, 0xDEADBEEF], dtype=torch.int64)
     for c in (rng.C_ROW, rng.C_COL, 0x85EBCA6B):
