@@ -218,6 +218,9 @@ __global__ __launch_bounds__(256) void norm_bwd_dx_kernel(
 // with K = (RMS ? 1 : 2) + DXSUM, summed into the gradient slots by colreduce_multi.  Replaces
 // norm_bwd_dx + a colpart launch.
 constexpr int kFusedWaves = 8;     // 512-thread blocks: two waves per SIMD at one block per CU
+// one-barrier fold while the K x 8 x d fp32 images fit (d <= 1024 at K = 3): -0.4 us per launch isolated,
+// profiles/norm_bwd_fold_ab_r6.txt
+constexpr size_t kFoldLdsMax = 128 * 1024;
 
 // XS (extra column sum): 0 none; 1 the stored dx; 2 the dropout backward of dx, dm = keep * dx / (1-p)
 // with the keep bits of dropout site `site` (bitwise the colpart DROP kernel's dm), stored to `dm`,
@@ -229,8 +232,9 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx, float* __restrict__ part, int N, int d,
     int rpw, bf16_t* __restrict__ dm, uint32_t thr16, float drop_scale, const int64_t* __restrict__ seed_ptr,
-    int64_t site) {
-  extern __shared__ __attribute__((aligned(16))) float fold[];   // [kFusedWaves][d]
+    int64_t site, bool one_fold) {
+  // [kFusedWaves][d], or [K][kFusedWaves][d] with one_fold (all partial images folded after one barrier)
+  extern __shared__ __attribute__((aligned(16))) float fold[];
   constexpr bool DXSUM = XS != 0;
   constexpr int K = (RMS ? 1 : 2) + (DXSUM ? 1 : 0);
   const uint64_t dseed = (XS == 2 && thr16) ? site_seed(seed_ptr, site) : 0ull;
@@ -318,6 +322,29 @@ __global__ __launch_bounds__(kFusedWaves * 64) void norm_bwd_fused_kernel(
         }
       }
     }
+  }
+  if (one_fold) {                                        // LDS holds all K images: one barrier
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < nvec) {
+          float4* f = reinterpret_cast<float4*>(fold + (k * kFusedWaves + wid) * d + idx * 8);
+          f[0] = make_float4(acc[k][j][0], acc[k][j][1], acc[k][j][2], acc[k][j][3]);
+          f[1] = make_float4(acc[k][j][4], acc[k][j][5], acc[k][j][6], acc[k][j][7]);
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      for (int c = threadIdx.x; c < d; c += kFusedWaves * 64) {
+        float t = 0.f;
+#pragma unroll
+        for (int v = 0; v < kFusedWaves; ++v) t += fold[(k * kFusedWaves + v) * d + c];
+        part[((size_t)k * gridDim.x + blockIdx.x) * d + c] = t;
+      }
+    return;
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -595,9 +622,20 @@ void launch_bwd_fused(int N, int d, hipStream_t st, const bf16_t* dy, const bf16
                       const float* mean, const float* rstd, const bf16_t* dres, bf16_t* dx, float* part,
                       const FusedDrop& fd) {
   const int rpw = dltb_norm_bwd_fused_rpw(N);
+  constexpr int K = (RMS ? 1 : 2) + (XS ? 1 : 0);
+  const size_t one = (size_t)K * kFusedWaves * d * sizeof(float);
+  const bool one_fold = one <= kFoldLdsMax;
+  if (one_fold && one > 65536) {
+    static bool attr = false;                 // per instantiation: allow the large dynamic LDS image
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)norm_bwd_fused_kernel<NV, RMS, RES, XS>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFoldLdsMax);
+      attr = true;
+    }
+  }
   hipLaunchKernelGGL((norm_bwd_fused_kernel<NV, RMS, RES, XS>), dim3(dltb_norm_bwd_fused_blocks(N)),
-                     dim3(kFusedWaves * 64), (size_t)kFusedWaves * d * sizeof(float), st, dy, s, w, mean, rstd, dres, dx,
-                     part, N, d, rpw, fd.dm, fd.thr16, fd.scale, fd.seed, fd.site);
+                     dim3(kFusedWaves * 64), one_fold ? one : (size_t)kFusedWaves * d * sizeof(float), st, dy, s, w,
+                     mean, rstd, dres, dx, part, N, d, rpw, fd.dm, fd.thr16, fd.scale, fd.seed, fd.site, one_fold);
 }
 template <int NV, bool RMS, bool RES>
 void launch_bwd_fused_xs(int xs, int N, int d, hipStream_t st, const bf16_t* dy, const bf16_t* s,
