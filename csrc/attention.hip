@@ -126,14 +126,22 @@ struct TileLoader {
 // column dt*32 + (i&3) + 8(i>>2) + 4h, scaled
 template <int D>
 DLTB_DEV void store_acc_rows(bf16_t* dst_row, const f32x16* acc, float scale, int h) {
+  // lanes r and r + 32 hold the two 4-column halves of each 8-column chunk of row r: one v_permlane32_swap per
+  // dword hands lane r the chunk of group g0 and lane r + 32 that of g0 + 1, so every lane stores 16 bytes
+  // (D / 16 dwordx4 stores instead of D / 8 dwordx2: the epilogue store tail is issue-bound).  All 64 lanes
+  // must be active (every caller stores from wave-uniform control flow).
 #pragma unroll
   for (int dt = 0; dt < D / 32; ++dt) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      uint2 o;
-      o.x = pack_bf2(acc[dt][4 * g + 0] * scale, acc[dt][4 * g + 1] * scale);
-      o.y = pack_bf2(acc[dt][4 * g + 2] * scale, acc[dt][4 * g + 3] * scale);
-      *reinterpret_cast<uint2*>(dst_row + dt * 32 + 8 * g + 4 * h) = o;
+    for (int g0 = 0; g0 < 4; g0 += 2) {
+      const uint32_t x0 = pack_bf2(acc[dt][4 * g0 + 0] * scale, acc[dt][4 * g0 + 1] * scale);
+      const uint32_t x1 = pack_bf2(acc[dt][4 * g0 + 2] * scale, acc[dt][4 * g0 + 3] * scale);
+      const uint32_t y0 = pack_bf2(acc[dt][4 * g0 + 4] * scale, acc[dt][4 * g0 + 5] * scale);
+      const uint32_t y1 = pack_bf2(acc[dt][4 * g0 + 6] * scale, acc[dt][4 * g0 + 7] * scale);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+      const uint4 o = {s0[0], s1[0], s0[1], s1[1]};
+      *reinterpret_cast<uint4*>(dst_row + dt * 32 + 8 * (g0 + h)) = o;
     }
   }
 }
